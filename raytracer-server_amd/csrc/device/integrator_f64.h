@@ -1,0 +1,142 @@
+// Per-vertex integrator shared by the megakernel and the wavefront shade kernel.
+//
+// The reference's recursion (scene.rs:152-244) restated as a forward walk with throughput:
+//   received_radiance(r)  = Le(x1) + R(x1, -d, 1)                                   (:152-159)
+//   R(x, o, k), mirror    = [u < p] ( Le(x') + R(x', o, k+1) * f cos / (pdf p) )    (:170-185)
+//   R(x, o, k), diffuse   = NEE(x, o) + [u < p] R(x', -i, k+1) * f cos / (pdf p)    (:217-242)
+// so, walking forward with beta = product of the weights so far:
+//   camera hit:  L  = Le(x1)
+//   mirror:      L += beta (.) Le(x'),  beta (.)= f cos / (pdf p)   (Le(x') is NOT weighted by
+//                this vertex's f cos / (pdf p) — exactly as in the reference expression)
+//   diffuse:     L += beta (.) NEE,     beta (.)= f cos / (pdf p)
+// `o` stays unchanged across a mirror bounce (the reference passes the same `o`, scene.rs:178).
+// Sums are taken in a different association than the recursion, so f64 results agree with the
+// recursive oracle to ~1e-15 relative, not bit for bit.
+#pragma once
+
+#include "../kernels/kernels.h"
+#include "path_f64.h"
+
+namespace rt {
+namespace f64 {
+
+enum : int { K_CAMERA = 0, K_SPEC = 1, K_DIFF = 2 };
+
+struct PathState {
+    Ray ray;
+    V3 beta, L, bemit, o;
+    double pdf_prev;
+    uint32_t depth;
+    int kind;
+};
+
+// Tile-local subpixel id -> pixel coordinates (RenderJob::run flips y, server.rs:181).
+struct SubPixel {
+    uint32_t pid;  // global pixel id (RNG key)
+    int col, yref, sx, sy, sub;
+};
+RT_DEV SubPixel subpixel_of(const RenderArgs& a, long p) {
+    long pix = p >> 2;
+    SubPixel s;
+    s.sub = (int)(p & 3);
+    s.col = a.x0 + (int)(pix % a.tw);
+    int row = a.y0 + (int)(pix / a.tw);
+    s.yref = a.height - row - 1;
+    s.pid = (uint32_t)row * (uint32_t)a.width + (uint32_t)s.col;
+    s.sx = s.sub & 1;
+    s.sy = s.sub >> 1;
+    return s;
+}
+
+// New camera path for sample `smp` of subpixel `sp` (server.rs:338-357).
+RT_DEV void begin_sample(const DevScene& sc, const RenderArgs& a, const SubPixel& sp, int smp, PathState& ps) {
+    Rng rng(a.seed, sp.pid, (uint32_t)smp, 0u, (uint32_t)sp.sub);
+    double u1 = rng.uniform(), u2 = rng.uniform();
+    ps.ray = camera_ray(sc, ld3(a.cx), ld3(a.cy), (double)a.width, (double)a.height, sp.col, sp.yref, sp.sx, sp.sy, u1, u2);
+    ps.beta = v3(1, 1, 1);
+    ps.L = v3(0, 0, 0);
+    ps.bemit = v3(0, 0, 0);
+    ps.o = v3(0, 0, 0);
+    ps.pdf_prev = 0.0;
+    ps.depth = 0;
+    ps.kind = K_CAMERA;
+}
+
+// Shades the hit `hr` of ps.ray. Returns true when the path continues (ps.ray is the next ray to
+// trace), false when this sample's radiance ps.L is final. The shadow ray of next-event estimation
+// is traced inline.
+RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, const SubPixel& sp, int smp, PathState& ps,
+                         const HitRec& hr) {
+    if (hr.obj < 0) return false;  // no hit: R = 0 (scene.rs:157, :175, :233)
+    const DevObject& obj = sc.objects[hr.obj];
+    V3 x, nrm;
+    surface(sc, ps.ray, hr, &x, &nrm);
+    if (ps.kind == K_CAMERA) {
+        ps.L = ld3(obj.emitted);
+    } else if (ps.kind == K_SPEC) {
+        ps.L = ps.L + mult(ps.bemit, ld3(obj.emitted));
+    } else if (a.mis && hr.obj == sc.light && ps.pdf_prev > 0.0) {
+        // MIS, BSDF strategy: emitted radiance with the balance-heuristic weight
+        double cosl = dot(nrm, -ps.ray.d);
+        double pdf_l = light_pdf_area(sc) * (hr.t * hr.t) / cosl;
+        double wgt = ps.pdf_prev / (ps.pdf_prev + pdf_l);
+        ps.L = ps.L + mult(ps.beta, ld3(obj.emitted) * wgt);
+    }
+    if (ps.kind != K_SPEC) ps.o = -ps.ray.d;
+    ps.depth += 1;
+    const double p = ps.depth <= (uint32_t)MAX_BOUNCES ? 1.0 : SURVIVAL_PROBABILITY;
+    Rng rng(a.seed, sp.pid, (uint32_t)smp, ps.depth, (uint32_t)sp.sub);
+    VertexDraws d;
+    if (obj.brdf == BRDF_SPECULAR) {
+        draw_vertex(rng, d, 3);
+        if (!(d.v[2] < p)) return false;
+        V3 i;
+        double pdf;
+        brdf_sample(obj, nrm, ps.o, d, &i, &pdf);
+        V3 f = brdf_eval(obj, nrm, ps.o, i);
+        ps.bemit = ps.beta;
+        ps.beta = mult(ps.beta, f) * dot(nrm, i) / (pdf * p);
+        ps.ray = Ray{x, i};
+        ps.kind = K_SPEC;
+        return true;
+    }
+    draw_vertex(rng, d, obj.brdf == BRDF_PHONG ? 6 : 5);
+    const bool use_mis = a.mis && obj.brdf == BRDF_DIFFUSE;
+    // next-event estimation (scene.rs:217-229)
+    V3 y, ny;
+    double pdfA;
+    light_sample(sc, d, &y, &ny, &pdfA);
+    V3 i = norm(y - x);
+    double r_sqr = dot(y - x, y - x);
+    V3 lef = mult(ld3(sc.objects[sc.light].emitted), brdf_eval(obj, nrm, ps.o, i));
+    if (!is_zero(lef)) {  // a zero Le*f makes the term exactly 0: skip the shadow ray
+        double vis = visible(sc, x, y) ? 1. : 0.;
+        V3 c;
+        if (!use_mis) {
+            c = lef * vis * dot(nrm, i) * dot(ny, -i) / (r_sqr * pdfA);
+        } else {
+            double cosl = dot(ny, -i);
+            double pdf_l = pdfA * r_sqr / cosl;
+            double pdf_b = dot(nrm, i) * FRAC_1_PI;
+            c = v3(0, 0, 0);
+            if (vis > 0. && cosl > 0. && pdf_b > 0.) c = lef * dot(nrm, i) * ((pdf_l / (pdf_l + pdf_b)) / pdf_l);
+        }
+        ps.L = ps.L + mult(ps.beta, c);
+    }
+    // Russian roulette + BSDF continuation (scene.rs:231-240)
+    if (!(d.v[2] < p)) return false;
+    V3 wi;
+    double pdf;
+    brdf_sample(obj, nrm, ps.o, d, &wi, &pdf);
+    V3 f = brdf_eval(obj, nrm, ps.o, wi);
+    ps.beta = mult(ps.beta, f) * dot(nrm, wi) / (pdf * p);
+    ps.ray = Ray{x, wi};
+    ps.kind = K_DIFF;
+    ps.pdf_prev = use_mis ? pdf : 0.0;
+    // zero throughput: every later term is exactly 0, and with a counter-based RNG no draws need
+    // to be kept in step — end the path (same result, less work)
+    return !is_zero(ps.beta);
+}
+
+}  // namespace f64
+}  // namespace rt

@@ -1,0 +1,421 @@
+// f64 device path: the reference's hot path (server.rs:320-368, scene.rs:30-289,
+// geometry.rs:512-670, 977-1036, 1237-1295) restated for CDNA4 lanes.
+//
+// Compiled with -ffp-contract=off: every expression keeps the reference's operation order, so a
+// lane produces the same f64 bits as the reference's arithmetic (and the oracle) except where
+// device libm (sin/cos/pow) differs by an ulp from the host's.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "scene_layout.h"
+
+namespace rt {
+namespace f64 {
+
+#define RT_DEV __device__ __forceinline__
+
+constexpr double PI = 3.14159265358979323846264338327950288;
+constexpr double FRAC_1_PI = 0.318309886183790671537767526745028724;
+constexpr int MAX_BOUNCES = 5;               // scene.rs:109
+constexpr double SURVIVAL_PROBABILITY = 0.9;  // scene.rs:110
+
+struct V3 {
+    double x, y, z;
+};
+RT_DEV V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+RT_DEV V3 ld3(const double* p) { return V3{p[0], p[1], p[2]}; }
+RT_DEV V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+RT_DEV V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+RT_DEV V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
+RT_DEV V3 operator*(V3 a, double s) { return v3(a.x * s, a.y * s, a.z * s); }
+RT_DEV V3 operator*(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
+RT_DEV V3 operator/(V3 a, double s) { return v3(a.x / s, a.y / s, a.z / s); }
+RT_DEV double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+RT_DEV V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+RT_DEV V3 mult(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+RT_DEV double mag(V3 a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+RT_DEV V3 norm(V3 a) { return a / mag(a); }
+RT_DEV bool equal_within(V3 a, V3 b, double e) {
+    return fabs(a.x - b.x) < e && fabs(a.y - b.y) < e && fabs(a.z - b.z) < e;
+}
+RT_DEV V3 flip_across(V3 a, V3 axis) { return (2.0 * dot(a, axis)) * axis - a; }
+RT_DEV bool is_zero(V3 a) { return a.x == 0.0 && a.y == 0.0 && a.z == 0.0; }
+RT_DEV double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+RT_DEV V3 clampv(V3 a, double lo, double hi) { return v3(clampd(a.x, lo, hi), clampd(a.y, lo, hi), clampd(a.z, lo, hi)); }
+RT_DEV double det3(V3 v0, V3 v1, V3 v2) {
+    return v0.x * (v1.y * v2.z - v1.z * v2.y) - v1.x * (v0.y * v2.z - v0.z * v2.y) + v2.x * (v0.y * v1.z - v0.z * v1.y);
+}
+RT_DEV double powi(double b, int n) {
+    bool neg = n < 0;
+    unsigned e = neg ? (unsigned)(-n) : (unsigned)n;
+    double r = 1.0;
+    while (e) {
+        if (e & 1u) r *= b;
+        b *= b;
+        e >>= 1;
+    }
+    return neg ? 1.0 / r : r;
+}
+
+struct Ray {
+    V3 o, d;
+};
+RT_DEV V3 eval(const Ray& r, double t) { return r.o + t * r.d; }
+
+// ---------------------------------------------------------------- RNG
+struct Rng {
+    uint64_t s0, s1;
+    RT_DEV Rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t depth, uint32_t sub) {
+        uint32_t c0 = pixel, c1 = sample, c2 = depth, c3 = sub;
+        uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+        for (int r = 0; r < 10; ++r) {
+            if (r) {
+                k0 += 0x9E3779B9u;
+                k1 += 0xBB67AE85u;
+            }
+            uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+            uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+            uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+            c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        }
+        s0 = ((uint64_t)c0 << 32) | c1;
+        s1 = ((uint64_t)c2 << 32) | c3;
+        if ((s0 | s1) == 0) s0 = 1;
+    }
+    static RT_DEV uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    RT_DEV uint64_t next() {  // xoroshiro128++
+        uint64_t a = s0, b = s1;
+        uint64_t r = rotl(a + b, 17) + a;
+        b ^= a;
+        s0 = rotl(a, 49) ^ b ^ (b << 21);
+        s1 = rotl(b, 28);
+        return r;
+    }
+    RT_DEV double uniform() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
+};
+// Draw slots (fixed per vertex so every kernel consumes them identically):
+// camera (depth 0): r1, r2; vertex: light xi1, xi2, RR, bsdf u1, u2, u3, light pick.
+struct VertexDraws {
+    double v[7];
+};
+RT_DEV void draw_vertex(Rng& r, VertexDraws& d, int n) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+        if (k < n) d.v[k] = r.uniform();
+}
+
+// ---------------------------------------------------------------- primitives (geometry.rs:512-571)
+RT_DEV bool sphere_t(const DevObject& o, const Ray& ray, double* tout) {
+    V3 op = ld3(o.pos) - ray.o;
+    const double eps = 1e-4;
+    double b = dot(op, ray.d);
+    double det = b * b - dot(op, op) + o.r * o.r;
+    if (det < 0.) return false;
+    det = sqrt(det);
+    double t = b - det;
+    if (t > eps) { *tout = t; return true; }
+    t = b + det;
+    if (t > eps) { *tout = t; return true; }
+    return false;
+}
+RT_DEV bool plane_t(const DevObject& o, const Ray& ray, double* tout) {
+    V3 n = ld3(o.n);
+    double dn = dot(ray.d, n);
+    if (fabs(dn) < 0.0001) return false;
+    double t = dot(ld3(o.pos) - ray.o, n) / dot(ray.d, n);
+    if (t >= 0.) { *tout = t; return true; }
+    return false;
+}
+// Triangle::intersect (geometry.rs:637-670) on the precomputed (a, ab, ac, n).
+RT_DEV bool tri_t(const DevTri& tr, const Ray& ray, double* tout) {
+    V3 n = ld3(tr.n);
+    if (fabs(dot(n, ray.d)) < 0.0001) return false;
+    V3 ab = ld3(tr.ab), ac = ld3(tr.ac);
+    V3 b = ray.o - ld3(tr.a);
+    V3 nd = -ray.d;
+    double det = det3(nd, ab, ac);
+    double t = det3(b, ab, ac) / det;
+    double u = det3(nd, b, ac) / det;
+    double v = det3(nd, ab, b) / det;
+    if (u < 0. || u > 1. || v < 0. || u + v > 1.) return false;
+    if (t > 0.0001) { *tout = t; return true; }
+    return false;
+}
+// BoundingBox::intersect(..).is_some() (geometry.rs:977-1036): first face in order (-x,+x,-y,+y,-z,+z).
+RT_DEV bool box_hit(const double* bx, const Ray& r) {
+    const double EPS = 0.0000001;
+    const double mnx = bx[0], mny = bx[1], mnz = bx[2], mxx = bx[3], mxy = bx[4], mxz = bx[5];
+    double t;
+    V3 p;
+    t = (mnx - r.o.x) / r.d.x;
+    if (t >= EPS) { p = eval(r, t); if (mny <= p.y && p.y <= mxy && mnz <= p.z && p.z <= mxz) return true; }
+    t = (mxx - r.o.x) / r.d.x;
+    if (t >= EPS) { p = eval(r, t); if (mny <= p.y && p.y <= mxy && mnz <= p.z && p.z <= mxz) return true; }
+    t = (mny - r.o.y) / r.d.y;
+    if (t >= EPS) { p = eval(r, t); if (mnx <= p.x && p.x <= mxx && mnz <= p.z && p.z <= mxz) return true; }
+    t = (mxy - r.o.y) / r.d.y;
+    if (t >= EPS) { p = eval(r, t); if (mnx <= p.x && p.x <= mxx && mnz <= p.z && p.z <= mxz) return true; }
+    t = (mnz - r.o.z) / r.d.z;
+    if (t >= EPS) { p = eval(r, t); if (mnx <= p.x && p.x <= mxx && mny <= p.y && p.y <= mxy) return true; }
+    t = (mxz - r.o.z) / r.d.z;
+    if (t >= EPS) { p = eval(r, t); if (mnx <= p.x && p.x <= mxx && mny <= p.y && p.y <= mxy) return true; }
+    return false;
+}
+
+// Leaf: nearest triangle, strict < (geometry.rs:1276-1293).
+RT_DEV bool leaf_hit(const DevScene& sc, int off, int cnt, const Ray& ray, double* t, int* prim) {
+    bool any = false;
+    for (int r = 0; r < cnt; ++r) {
+        int ti = sc.tri_ref[off + r];
+        double tt;
+        if (tri_t(sc.tris[ti], ray, &tt)) {
+            if (!any || tt < *t) { *t = tt; *prim = ti; any = true; }
+        }
+    }
+    return any;
+}
+
+// Octree::intersect (geometry.rs:1237-1295), stackless: the per-ray child order (root-octant
+// centre distances, insertion-sorted, strict >) is identical at every level, so the DFS resumes
+// from parent links + the child's slot rank instead of a stack. Same visiting order and the same
+// first-leaf-with-a-hit exit as the reference recursion; no per-lane stack memory.
+RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, double* t, int* prim) {
+    if (m.n_nodes == 0) return false;
+    const int root = m.node_base;
+    NodeMeta rm = sc.node_meta[root];
+    if (rm.leaf_off >= 0) return leaf_hit(sc, rm.leaf_off, rm.leaf_cnt, ray, t, prim);
+    double dist[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dist[i] = mag(ld3(m.oct_center[i]) - ray.o);
+    uint32_t order = 0x76543210u;  // nibble k = octant visited k-th
+#pragma unroll
+    for (int i = 1; i < 8; ++i) {
+#pragma unroll
+        for (int j = i; j > 0; --j) {
+            int a = (order >> (4 * (j - 1))) & 0xF, b = (order >> (4 * j)) & 0xF;
+            // insertion sort step (swap while strictly greater); unrolled as bubble passes with the
+            // same comparisons: stop condition emulated by the monotone prefix property.
+            if (dist[a] > dist[b]) {
+                order &= ~((0xFu << (4 * (j - 1))) | (0xFu << (4 * j)));
+                order |= ((uint32_t)b << (4 * (j - 1))) | ((uint32_t)a << (4 * j));
+            } else {
+                break;
+            }
+        }
+    }
+    uint32_t rank = 0;  // nibble i = position of octant i in `order`
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rank |= (uint32_t)k << (4 * ((order >> (4 * k)) & 0xF));
+
+    int cur = root;
+    int k = 0;
+    while (true) {
+        int found = -1;
+        const int* ch = sc.node_child + 8 * (size_t)cur;
+        for (; k < 8; ++k) {
+            int oi = (order >> (4 * k)) & 0xF;
+            int c = ch[oi];
+            if (c >= 0 && box_hit(sc.node_box + 6 * (size_t)c, ray)) { found = c; break; }
+        }
+        if (found >= 0) {
+            NodeMeta fm = sc.node_meta[found];
+            if (fm.leaf_off >= 0) {
+                if (leaf_hit(sc, fm.leaf_off, fm.leaf_cnt, ray, t, prim)) return true;
+                ++k;  // next sibling
+            } else {
+                cur = found;
+                k = 0;
+            }
+            continue;
+        }
+        if (cur == root) return false;
+        NodeMeta cm = sc.node_meta[cur];
+        k = (int)((rank >> (4 * cm.slot)) & 0xF) + 1;
+        cur = cm.parent;
+    }
+}
+
+// One object's Geometry::intersect, reporting t (and the triangle for meshes).
+RT_DEV bool object_t(const DevScene& sc, const DevObject& o, const Ray& ray, double* t, int* prim) {
+    if (o.geom == GEOM_SPHERE) return sphere_t(o, ray, t);
+    if (o.geom == GEOM_PLANE) return plane_t(o, ray, t);
+    return mesh_hit(sc, sc.meshes[o.mesh], ray, t, prim);
+}
+
+struct HitRec {
+    double t;
+    int obj;   // -1: no hit
+    int prim;  // triangle (meshes)
+};
+
+// Scene::trace_ray (scene.rs:272-289): nearest over all objects, ties to the lower index.
+RT_DEV HitRec trace_closest(const DevScene& sc, const Ray& ray) {
+    HitRec h{0.0, -1, -1};
+    for (int i = 0; i < sc.n_objects; ++i) {
+        const DevObject& o = sc.objects[i];
+        double t;
+        int prim = -1;
+        if (object_t(sc, o, ray, &t, &prim)) {
+            if (h.obj < 0 || t < h.t) { h.t = t; h.obj = i; h.prim = prim; }
+        }
+    }
+    return h;
+}
+
+// Hit position and facing normal, computed exactly as the intersect routines build their Hit.
+RT_DEV void surface(const DevScene& sc, const Ray& ray, const HitRec& h, V3* pos, V3* n) {
+    const DevObject& o = sc.objects[h.obj];
+    if (o.geom == GEOM_SPHERE) {
+        V3 p = eval(ray, h.t);
+        V3 nn = norm(p - ld3(o.pos));
+        *pos = p;
+        *n = dot(nn, -ray.d) >= 0. ? nn : -nn;
+    } else if (o.geom == GEOM_PLANE) {
+        V3 pn = ld3(o.n);
+        V3 nn = dot(pn, -ray.d) >= 0. ? pn : -pn;
+        *pos = eval(ray, h.t) + nn * 0.00001;
+        *n = nn;
+    } else {
+        V3 tn = ld3(sc.tris[h.prim].n);
+        V3 nn = dot(tn, -ray.d) >= 0. ? tn : -tn;
+        *pos = eval(ray, h.t) + 0.00001 * nn;
+        *n = nn;
+    }
+}
+
+// Scene::mutually_visible (scene.rs:258-270) as an any-hit query: occluded iff some object's
+// intersect t satisfies t + 0.001 < |y - x| (equivalent to the nearest-hit test because x + 0.001
+// rounds monotonically). Analytic objects are tested before meshes (order-free for a boolean).
+RT_DEV bool visible(const DevScene& sc, V3 x, V3 y) {
+    const double ERR_MARGIN = 0.001;
+    V3 diff = y - x;
+    Ray r{x, norm(diff)};
+    double dist = mag(diff);
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int i = 0; i < sc.n_objects; ++i) {
+            const DevObject& o = sc.objects[i];
+            if ((o.geom == GEOM_MESH) != (pass == 1)) continue;
+            double t;
+            int prim;
+            if (object_t(sc, o, r, &t, &prim) && !(t + ERR_MARGIN >= dist)) return false;
+        }
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------- BRDF (scene.rs:30-123)
+RT_DEV V3 brdf_eval(const DevObject& o, V3 n, V3 out, V3 in) {
+    if (o.brdf == BRDF_DIFFUSE) return ld3(o.k) * FRAC_1_PI;
+    if (o.brdf == BRDF_SPECULAR) {
+        if (equal_within(in, flip_across(out, n), 0.001)) return ld3(o.k) / dot(n, in);
+        return v3(0, 0, 0);
+    }
+    V3 refl = flip_across(in, n);
+    double c = fmax(dot(out, refl), 0.);
+    return ld3(o.color_d) * o.ph_kd * FRAC_1_PI +
+           ld3(o.color_s) * o.ph_ks * (double)(o.ph_power + 2) / (2. * PI) * powi(c, o.ph_power);
+}
+RT_DEV void local_coord(V3 n, V3* u, V3* v, V3* w) {
+    *w = n;
+    V3 base = fabs(w->x) > 0.1 ? v3(0., 1., 0.) : v3(1., 0., 0.);
+    *u = norm(cross(base, *w));
+    *v = cross(*w, *u);
+}
+// sample_incoming (scene.rs:56-98); draws: u1 = d[3], u2 = d[4], u3 = d[5].
+RT_DEV void brdf_sample(const DevObject& o, V3 n, V3 out, const VertexDraws& d, V3* in, double* pdf) {
+    if (o.brdf == BRDF_DIFFUSE) {
+        double z = sqrt(d.v[3]);
+        double r = sqrt(1.0 - z * z);
+        double phi = 2.0 * PI * d.v[4];
+        double x = r * cos(phi), y = r * sin(phi);
+        V3 u, v, w;
+        local_coord(n, &u, &v, &w);
+        V3 i = norm(u * x + v * y + w * z);
+        *in = i;
+        *pdf = dot(n, i) * FRAC_1_PI;
+        return;
+    }
+    if (o.brdf == BRDF_SPECULAR) {
+        *in = flip_across(out, n);
+        *pdf = 1.0;
+        return;
+    }
+    double p = (double)o.ph_power;
+    double u = d.v[3];
+    if (u < o.ph_kd) {
+        double xi1 = d.v[4], xi2 = d.v[5];
+        V3 i = v3(sqrt(1. - xi1) * cos(2. * PI * xi2), sqrt(1. - xi1) * sin(2. * PI * xi2), sqrt(xi1));
+        *in = i;
+        *pdf = dot(n, i) * FRAC_1_PI;
+    } else if (o.ph_kd <= u && u < o.ph_kd + o.ph_ks) {
+        double xi1 = d.v[4], xi2 = d.v[5];
+        V3 i = v3(sqrt(1. - pow(xi1, 2. / (p + 1.))) * cos(2. * PI * xi2),
+                  sqrt(1. - pow(xi1, 2. / (p + 1.))) * sin(2. * PI * xi2), pow(xi1, 1. / (p + 1.)));
+        *in = i;
+        *pdf = (p + 1.) / (2. * PI) * powi(i.z, o.ph_power);
+    } else {
+        *in = v3(0, 0, 0);
+        *pdf = 1.0;
+    }
+}
+
+// ---------------------------------------------------------------- light (geometry.rs:573-595)
+RT_DEV void light_sample(const DevScene& sc, const VertexDraws& d, V3* y, V3* ny, double* pdf) {
+    const DevObject& L = sc.objects[sc.light];
+    if (L.geom == GEOM_SPHERE) {
+        double xi1 = d.v[0], xi2 = d.v[1];
+        double z = 2. * xi1 - 1.;
+        double x = sqrt(1.0 - z * z) * cos(2. * PI * xi2);
+        double yy = sqrt(1.0 - z * z) * sin(2. * PI * xi2);
+        V3 n = norm(v3(x, yy, z));
+        *y = ld3(L.pos) + n * L.r;
+        *ny = n;
+        *pdf = 1.0 / (4.0 * PI * L.r * L.r);
+        return;
+    }
+    // mesh light: area-weighted pick + Triangle::sample with the reference's missing `+ a`
+    const DevMesh& m = sc.meshes[L.mesh];
+    double u = d.v[6] * m.total_weight;
+    int lo = 0, hi = m.n_tris - 1;  // first triangle whose cumulative area > u
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (sc.tri_cum_area[m.tri_base + mid] > u) hi = mid;
+        else lo = mid + 1;
+    }
+    const DevTri& t = sc.tris[m.tri_base + lo];
+    double b0 = 1. - sqrt(d.v[0]);
+    double b1 = (1. - b0) * d.v[1];
+    V3 ab = norm(ld3(t.ab)), ac = norm(ld3(t.ac));
+    *y = ab * b0 + ac * b1;
+    *ny = ld3(t.n);
+    *pdf = 1. / m.surface_area;
+}
+RT_DEV double light_pdf_area(const DevScene& sc) {
+    const DevObject& L = sc.objects[sc.light];
+    if (L.geom == GEOM_SPHERE) return 1.0 / (4.0 * PI * L.r * L.r);
+    return 1. / sc.meshes[L.mesh].surface_area;
+}
+
+// Camera ray of server.rs:339-357 for subpixel (sx, sy) of pixel (x, y_ref).
+RT_DEV Ray camera_ray(const DevScene& sc, V3 cx, V3 cy, double w, double h, int x, int y, int sx, int sy, double u1,
+                      double u2) {
+    double r1 = 2. * u1;
+    double dx = r1 < 1. ? sqrt(r1) - 1. : 1. - sqrt(2. - r1);
+    double r2 = 2. * u2;
+    double dy = r2 < 1. ? sqrt(r2) - 1. : 1. - sqrt(2. - r2);
+    V3 d = cx * ((((double)sx + 0.5 + dx) / 2. + (double)x) / w - 0.5) +
+           cy * ((((double)sy + 0.5 + dy) / 2. + (double)y) / h - 0.5) + ld3(sc.cam_dir);
+    return Ray{ld3(sc.cam_pos), norm(d)};
+}
+
+RT_DEV uint8_t as_u8(double v) {  // Rust `as u8`: saturating, NaN -> 0
+    if (!(v > 0.)) return 0;
+    if (v >= 255.) return 255;
+    return (uint8_t)v;
+}
+
+}  // namespace f64
+}  // namespace rt

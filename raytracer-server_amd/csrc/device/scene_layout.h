@@ -1,0 +1,66 @@
+// Device-resident scene layout (shared by the host packer and the HIP kernels).
+//
+// Everything is flat, read-only, and lives in HBM for the lifetime of an rt_scene; per-render
+// state (path slots, queues, accumulators) is allocated separately. f64 throughout, because the
+// reference is f64 (geometry.rs:21-26) and the default render mode is bit-faithful to it.
+#pragma once
+
+#include <stdint.h>
+
+namespace rt {
+
+enum : int32_t { GEOM_SPHERE = 0, GEOM_PLANE = 1, GEOM_MESH = 2 };
+enum : int32_t { BRDF_DIFFUSE = 0, BRDF_SPECULAR = 1, BRDF_PHONG = 2 };
+
+// One scene object (scene.rs:10-15). 16-byte aligned so the uniform object loop reads it with
+// scalar (s_load) instructions.
+struct alignas(16) DevObject {
+    int32_t geom, brdf, mesh, ph_power;
+    double emitted[3];
+    double k[3];          // Diffuse kd / Specular ks
+    double pos[3];        // sphere centre / plane point
+    double r;             // sphere radius
+    double n[3];          // plane normal
+    double ph_kd, ph_ks;
+    double color_d[3], color_s[3];
+    int32_t emissive, pad0, pad1, pad2;  // emitted != 0 (any component)
+};
+
+// Octree of one mesh, flattened in the reference's DFS pre-order (geometry.rs:1164-1216) so node
+// i here is node i of the reference's Vec<Node>. Indices in node_child / tri_ref are GLOBAL
+// (mesh bases already added).
+struct alignas(16) DevMesh {
+    int32_t node_base, n_nodes, ref_base, n_refs;
+    int32_t tri_base, n_tris, pad0, pad1;
+    double root_box[6];       // Octree.bounding_box (min xyz, max xyz)
+    double oct_center[8][3];  // centres of the ROOT box's octants: traversal order key (geometry.rs:1249-1260)
+    double surface_area;      // Mesh.surface_area (mesh-light pdf, geometry.rs:591)
+    double total_weight;      // sum of triangle areas (WeightedIndex total)
+};
+
+// Per node: x = leaf tri_ref offset (-1 for a parent), y = leaf count, z = parent node (-1 root),
+// w = octant slot in the parent.
+struct alignas(16) NodeMeta {
+    int32_t leaf_off, leaf_cnt, parent, slot;
+};
+
+// Triangle, precomputed exactly as Triangle::intersect derives it per call (geometry.rs:637-653):
+// a, ab = b - a, ac = c - a, n = ((c - a) x (b - a)).norm(). 12 doubles = 96 B.
+struct DevTri {
+    double a[3], ab[3], ac[3], n[3];
+};
+
+struct DevScene {
+    const DevObject* objects;
+    const DevMesh* meshes;
+    const NodeMeta* node_meta;
+    const int32_t* node_child;  // [node][8], -1 = empty octant
+    const double* node_box;     // [node][6]
+    const int32_t* tri_ref;     // leaf triangle lists
+    const DevTri* tris;
+    const double* tri_cum_area;  // per triangle, cumulative area within its mesh (mesh-light pick)
+    int32_t n_objects, light, n_meshes, mesh_order_last;  // mesh_order_last: test meshes after analytic objects
+    double cam_pos[3], cam_dir[3];
+};
+
+}  // namespace rt

@@ -1,0 +1,27 @@
+// Host-visible launchers of the HIP kernels (implemented in *.hip, called by rt_api.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../device/scene_layout.h"
+
+namespace rt {
+
+struct RenderArgs {
+    int32_t width, height, x0, y0, tw, th;
+    int32_t n_samples;  // spp / 4 per subpixel
+    int32_t mis;
+    uint64_t seed;
+    double cx[3], cy[3];  // camera frame (server.rs:330-331), computed on the host
+    double inv_n;         // 1.0 / n_samples (server.rs:358)
+    double* sub_out;      // optional [pix][4][3]
+    uint8_t* rgb_out;     // [pix][3]
+    unsigned long long* counters;  // optional [0] = path vertices
+};
+
+hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, hipStream_t st);
+hipError_t launch_trace_f64(const DevScene& sc, long n, const double* o, const double* d, double* t, int32_t* obj,
+                            double* pos, double* nrm, hipStream_t st);
+
+}  // namespace rt

@@ -1,0 +1,349 @@
+// Streaming wavefront path tracer (f64) for gfx950.
+//
+// One bounce = two kernels over a dense SoA path stream (ping-pong A -> B):
+//   k_wf_extend : Scene::trace_ray of every live path's ray (scene.rs:272-289) -> hit (t, obj, prim)
+//   k_wf_shade  : emission, next-event estimation (shadow ray traced inline), Russian roulette and
+//                 BSDF sampling (scene.rs:161-244); finished samples are added to their subpixel
+//                 mean in sample order and immediately replaced by the subpixel's next sample, or
+//                 by a fresh subpixel from a global work counter (regeneration). Survivors and
+//                 regenerated paths are compacted into stream B: wave ballot -> popcount prefix ->
+//                 one atomicAdd per wave, every lane writing its state at base + prefix.
+// Streams never hold two live paths of one subpixel, so each subpixel's mean is a sequential sum
+// in sample order (identical to server.rs:338-358) with no atomics on the accumulator.
+// k_wf_finalize turns the 4 subpixel means of each pixel into RGB8 (server.rs:360-368).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "../device/integrator_f64.h"
+#include "wavefront.h"
+
+namespace rt {
+using namespace f64;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+RT_DEV void store_state(const PathStream& S, long i, const PathState& ps, int sub, int smp, bool mis) {
+    S.ox[i] = ps.ray.o.x; S.oy[i] = ps.ray.o.y; S.oz[i] = ps.ray.o.z;
+    S.dx[i] = ps.ray.d.x; S.dy[i] = ps.ray.d.y; S.dz[i] = ps.ray.d.z;
+    S.bx[i] = ps.beta.x; S.by[i] = ps.beta.y; S.bz[i] = ps.beta.z;
+    S.lx[i] = ps.L.x; S.ly[i] = ps.L.y; S.lz[i] = ps.L.z;
+    if (ps.kind == K_SPEC) {  // only a mirror bounce carries `o` and the emission weight forward
+        S.ex[i] = ps.bemit.x; S.ey[i] = ps.bemit.y; S.ez[i] = ps.bemit.z;
+        S.wx[i] = ps.o.x; S.wy[i] = ps.o.y; S.wz[i] = ps.o.z;
+    }
+    if (mis) S.pdf[i] = ps.pdf_prev;
+    S.sub[i] = sub;
+    S.sample[i] = smp;
+    S.dk[i] = (int32_t)((ps.depth << 2) | (uint32_t)ps.kind);
+}
+
+RT_DEV void load_state(const PathStream& S, long i, PathState& ps, int* sub, int* smp, bool mis) {
+    ps.ray.o = v3(S.ox[i], S.oy[i], S.oz[i]);
+    ps.ray.d = v3(S.dx[i], S.dy[i], S.dz[i]);
+    ps.beta = v3(S.bx[i], S.by[i], S.bz[i]);
+    ps.L = v3(S.lx[i], S.ly[i], S.lz[i]);
+    int32_t dk = S.dk[i];
+    ps.kind = dk & 3;
+    ps.depth = (uint32_t)dk >> 2;
+    if (ps.kind == K_SPEC) {
+        ps.bemit = v3(S.ex[i], S.ey[i], S.ez[i]);
+        ps.o = v3(S.wx[i], S.wy[i], S.wz[i]);
+    } else {
+        ps.bemit = v3(0, 0, 0);
+        ps.o = v3(0, 0, 0);
+    }
+    ps.pdf_prev = mis ? S.pdf[i] : 0.0;
+    *sub = S.sub[i];
+    *smp = S.sample[i];
+}
+
+// Wave-aggregated append: returns this lane's slot (valid only where pred).
+RT_DEV long wave_append(uint32_t* counter, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    if (m == 0ull) return -1;
+    const int lane = __lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+    return pred ? (long)base + __popcll(below) : -1;
+}
+
+__global__ __launch_bounds__(kBlock) void k_wf_init(DevScene sc, RenderArgs a, PathStream A, uint32_t* ctrl,
+                                                     long nsub, long slots, double* sub_buf) {
+    const long n0 = nsub < slots ? nsub : slots;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n0; i += stride) {
+        SubPixel sp = subpixel_of(a, i);
+        PathState ps;
+        begin_sample(sc, a, sp, 0, ps);
+        store_state(A, i, ps, (int)i, 0, a.mis != 0);
+    }
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nsub * 3; i += stride) sub_buf[i] = 0.0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctrl[0] = (uint32_t)n0;
+        ctrl[1] = 0;
+        ctrl[2] = (uint32_t)n0;  // next subpixel to hand out
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_wf_extend(DevScene sc, PathStream A, const uint32_t* cnt_in,
+                                                       uint32_t* cnt_out, double* __restrict__ ht,
+                                                       int32_t* __restrict__ hobj, int32_t* __restrict__ hprim) {
+    const long n = (long)*cnt_in;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_out = 0;  // stream B is refilled by k_wf_shade
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        Ray r{v3(A.ox[i], A.oy[i], A.oz[i]), v3(A.dx[i], A.dy[i], A.dz[i])};
+        HitRec h = trace_closest(sc, r);
+        ht[i] = h.t;
+        hobj[i] = h.obj;
+        hprim[i] = h.prim;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, PathStream A, PathStream B,
+                                                      const uint32_t* cnt_in, uint32_t* cnt_out, uint32_t* next_sub,
+                                                      long nsub, const double* __restrict__ ht,
+                                                      const int32_t* __restrict__ hobj,
+                                                      const int32_t* __restrict__ hprim, double* sub_buf,
+                                                      unsigned long long* counters) {
+    const long n = (long)*cnt_in;
+    const long stride = (long)gridDim.x * blockDim.x;
+    const bool mis = a.mis != 0;
+    unsigned long long nverts = 0;
+    // uniform trip count per wave: every lane reaches wave_append
+    for (long base = (long)blockIdx.x * blockDim.x; base < n; base += stride) {
+        const long i = base + threadIdx.x;
+        const bool active = i < n;
+        PathState ps;
+        int sub = 0, smp = 0;
+        bool emit = false;
+        if (active) {
+            load_state(A, i, ps, &sub, &smp, mis);
+            HitRec hr{ht[i], hobj[i], hprim[i]};
+            nverts += hr.obj >= 0;
+            SubPixel sp = subpixel_of(a, sub);
+            emit = shade_vertex(sc, a, sp, smp, ps, hr);
+            if (!emit) {
+                // sample finished: sequential mean update (server.rs:357-358), then regenerate
+                double* acc = sub_buf + (size_t)sub * 3;
+                acc[0] = acc[0] + ps.L.x * a.inv_n;
+                acc[1] = acc[1] + ps.L.y * a.inv_n;
+                acc[2] = acc[2] + ps.L.z * a.inv_n;
+                ++smp;
+                if (smp >= a.n_samples) {
+                    long nxt = (long)atomicAdd(next_sub, 1u);
+                    sub = (int)nxt;
+                    smp = 0;
+                    if (nxt < nsub) {
+                        sp = subpixel_of(a, nxt);
+                        begin_sample(sc, a, sp, 0, ps);
+                        emit = true;
+                    }
+                } else {
+                    begin_sample(sc, a, sp, smp, ps);
+                    emit = true;
+                }
+            }
+        }
+        long pos = wave_append(cnt_out, emit);
+        if (emit) store_state(B, pos, ps, sub, smp, mis);
+    }
+    if (counters) {
+        unsigned long long v = nverts;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(counters, v);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_wf_finalize(RenderArgs a, const double* __restrict__ sub_buf) {
+    const long npix = (long)a.tw * a.th;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += stride) {
+        const double* s = sub_buf + (size_t)p * 12;
+        V3 pixel = v3(0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pixel = pixel + clampv(v3(s[3 * j], s[3 * j + 1], s[3 * j + 2]), 0., 1.) * 0.25;
+        V3 c = clampv(pixel, 0., 1.);
+        const double g = 1.0 / 2.2;
+        V3 gc = v3(pow(c.x, g), pow(c.y, g), pow(c.z, g)) * 255.0 + v3(0.5, 0.5, 0.5);
+        a.rgb_out[p * 3 + 0] = as_u8(gc.x);
+        a.rgb_out[p * 3 + 1] = as_u8(gc.y);
+        a.rgb_out[p * 3 + 2] = as_u8(gc.z);
+    }
+}
+
+size_t env_size(const char* name, size_t dflt) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    long long x = std::atoll(v);
+    return x > 0 ? (size_t)x : dflt;
+}
+
+}  // namespace
+
+hipError_t Workspace::ensure_counters() {
+    if (counters) return hipSuccess;
+    hipError_t e = hipMalloc(&counters, 64);
+    if (e != hipSuccess) counters = nullptr;
+    return e;
+}
+
+hipError_t Workspace::ensure_sub(size_t pixels) {
+    if (sub_cap >= pixels) return hipSuccess;
+    if (sub_buf) (void)hipFree(sub_buf);
+    sub_buf = nullptr;
+    sub_cap = 0;
+    hipError_t e = hipMalloc(&sub_buf, pixels * 12 * sizeof(double));
+    if (e == hipSuccess) sub_cap = pixels;
+    return e;
+}
+
+hipError_t Workspace::ensure_slots(size_t n) {
+    hipError_t e;
+    if (!ctrl) {
+        e = hipMalloc(&ctrl, 64);
+        if (e != hipSuccess) return e;
+        e = hipHostMalloc((void**)&host_ctrl, 64, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    if (slots >= n) return hipSuccess;
+    if (blob) (void)hipFree(blob);
+    blob = nullptr;
+    slots = 0;
+    // per stream: 19 f64 arrays + 3 i32 arrays; hit: f64 + 2 i32
+    const size_t per_stream = n * (19 * sizeof(double) + 3 * sizeof(int32_t));
+    const size_t hits = n * (sizeof(double) + 2 * sizeof(int32_t));
+    const size_t pad = 64 * 1024;
+    e = hipMalloc(&blob, 2 * per_stream + hits + pad);
+    if (e != hipSuccess) { blob = nullptr; return e; }
+    char* p = (char*)blob;
+    auto take = [&](size_t bytes) {
+        char* r = p;
+        p += (bytes + 255) / 256 * 256;
+        return r;
+    };
+    for (int k = 0; k < 2; ++k) {
+        PathStream& S = s[k];
+        double** f[] = {&S.ox, &S.oy, &S.oz, &S.dx, &S.dy, &S.dz, &S.bx, &S.by, &S.bz, &S.lx,
+                        &S.ly, &S.lz, &S.ex, &S.ey, &S.ez, &S.wx, &S.wy, &S.wz, &S.pdf};
+        for (double** q : f) *q = (double*)take(n * sizeof(double));
+        S.sub = (int32_t*)take(n * sizeof(int32_t));
+        S.sample = (int32_t*)take(n * sizeof(int32_t));
+        S.dk = (int32_t*)take(n * sizeof(int32_t));
+    }
+    hit_t = (double*)take(n * sizeof(double));
+    hit_obj = (int32_t*)take(n * sizeof(int32_t));
+    hit_prim = (int32_t*)take(n * sizeof(int32_t));
+    slots = n;
+    return hipSuccess;
+}
+
+Workspace::~Workspace() {
+    if (counters) (void)hipFree(counters);
+    if (blob) (void)hipFree(blob);
+    if (ctrl) (void)hipFree(ctrl);
+    if (sub_buf) (void)hipFree(sub_buf);
+    if (host_ctrl) (void)hipHostFree(host_ctrl);
+    if (ev) (void)hipEventDestroy(ev);
+}
+
+int wavefront_render_f64(const DevScene& sc, const RenderArgs& a_in, Workspace& ws, hipStream_t st,
+                         const volatile int32_t* cancel, rt_render_stats* stats, std::string* err) {
+    RenderArgs a = a_in;
+    const long npix = (long)a.tw * a.th;
+    if (npix == 0) return RT_OK;
+    auto hip_fail = [&](hipError_t e, const char* what) {
+        *err = std::string(what) + ": " + hipGetErrorString(e);
+        return e == hipErrorOutOfMemory ? RT_E_OOM : RT_E_HIP;
+    };
+    hipError_t e;
+    double* sub_buf = a.sub_out;
+    if (!sub_buf) {
+        if ((e = ws.ensure_sub((size_t)npix)) != hipSuccess) return hip_fail(e, "subpixel buffer");
+        sub_buf = ws.sub_buf;
+    }
+    if ((e = ws.ensure_counters()) != hipSuccess) return hip_fail(e, "counters");
+    if (stats && (e = hipMemsetAsync(ws.counters, 0, 64, st)) != hipSuccess) return hip_fail(e, "counters");
+    const long nsub = npix * 4;
+    const size_t slots = std::min<size_t>((size_t)nsub, env_size("RT_WF_SLOTS", (size_t)1 << 21));
+    if ((e = ws.ensure_slots(slots)) != hipSuccess) return hip_fail(e, "path streams");
+
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const long grid_cap = (long)ncu * (long)env_size("RT_WF_BLOCKS_PER_CU", 8);
+    const long grid = std::max<long>(1, std::min<long>(grid_cap, ((long)slots + kBlock - 1) / kBlock));
+    const int batch = (int)env_size("RT_WF_BATCH", 16);
+
+    int64_t iters = 0;
+    if (a.n_samples > 0) {
+        hipLaunchKernelGGL(k_wf_init, dim3((unsigned)grid), dim3(kBlock), 0, st, sc, a, ws.s[0], ws.ctrl, nsub,
+                           (long)slots, sub_buf);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "k_wf_init");
+        int cur = 0;
+        bool pending = false;
+        while (true) {
+            for (int k = 0; k < batch; ++k) {
+                const int nxt = cur ^ 1;
+                hipLaunchKernelGGL(k_wf_extend, dim3((unsigned)grid), dim3(kBlock), 0, st, sc, ws.s[cur],
+                                   ws.ctrl + cur, ws.ctrl + nxt, ws.hit_t, ws.hit_obj, ws.hit_prim);
+                hipLaunchKernelGGL(k_wf_shade, dim3((unsigned)grid), dim3(kBlock), 0, st, sc, a, ws.s[cur], ws.s[nxt],
+                                   ws.ctrl + cur, ws.ctrl + nxt, ws.ctrl + 2, nsub, ws.hit_t, ws.hit_obj,
+                                   ws.hit_prim, sub_buf, stats ? ws.counters : nullptr);
+                cur = nxt;
+                ++iters;
+            }
+            if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "wavefront launch");
+            // Termination check one batch behind: read the live count written by the previous
+            // batch while this batch runs.
+            if (pending) {
+                if ((e = hipEventSynchronize(ws.ev)) != hipSuccess) return hip_fail(e, "wavefront sync");
+                if (ws.host_ctrl[0] == 0 && ws.host_ctrl[1] == 0) break;
+            }
+            // safety net: RR (p = 0.9 past depth 5) makes 10^5 bounces per sample unreachable
+            if (iters > (int64_t)a.n_samples * 4 * 100000 + 1000000) {
+                *err = "wavefront did not drain (iteration cap reached)";
+                return RT_E_HIP;
+            }
+            if (cancel && *cancel) {
+                (void)hipStreamSynchronize(st);
+                return RT_CANCELLED;
+            }
+            if ((e = hipMemcpyAsync(ws.host_ctrl, ws.ctrl, 16, hipMemcpyDeviceToHost, st)) != hipSuccess)
+                return hip_fail(e, "ctrl readback");
+            if ((e = hipEventRecord(ws.ev, st)) != hipSuccess) return hip_fail(e, "event");
+            pending = true;
+        }
+    }
+    if (a.n_samples <= 0) {
+        if ((e = hipMemsetAsync(sub_buf, 0, (size_t)npix * 12 * sizeof(double), st)) != hipSuccess)
+            return hip_fail(e, "memset");
+    }
+    const long fgrid = std::max<long>(1, std::min<long>(grid_cap, (npix + kBlock - 1) / kBlock));
+    hipLaunchKernelGGL(k_wf_finalize, dim3((unsigned)fgrid), dim3(kBlock), 0, st, a, (const double*)sub_buf);
+    if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "k_wf_finalize");
+    if (stats) {
+        unsigned long long c[1] = {0};
+        if ((e = hipMemcpyAsync(c, ws.counters, sizeof c, hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_fail(e, "stats");
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "stats sync");
+        stats->vertices = (int64_t)c[0];
+        stats->iterations = iters;
+        stats->kernel_launches[0] = iters;
+        stats->kernel_launches[1] = iters;
+    }
+    return RT_OK;
+}
+
+}  // namespace rt

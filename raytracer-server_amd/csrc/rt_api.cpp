@@ -1,0 +1,488 @@
+// C ABI (include/rt_ffi.h): scene packing + per-device upload, render dispatch, error reporting.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_ffi.h"
+#include "device/scene_layout.h"
+#include "host/scene_host.hpp"
+#include "kernels/kernels.h"
+#include "kernels/wavefront.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(e_ == hipErrorOutOfMemory ? RT_E_OOM : RT_E_HIP,                        \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                    \
+    } while (0)
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Host image of the device scene, packed once per scene.
+struct Packed {
+    std::vector<rt::DevObject> objects;
+    std::vector<rt::DevMesh> meshes;
+    std::vector<rt::NodeMeta> meta;
+    std::vector<int32_t> child;
+    std::vector<double> box;
+    std::vector<int32_t> refs;
+    std::vector<rt::DevTri> tris;
+    std::vector<double> cum_area;
+};
+
+struct DeviceCopy {
+    bool ready = false;
+    void* blob = nullptr;
+    rt::DevScene ds{};
+};
+
+}  // namespace
+
+struct rt_scene {
+    rt::host::Scene host;
+    Packed packed;
+    std::mutex mu;
+    std::vector<DeviceCopy> dev;
+    std::vector<std::unique_ptr<rt::Workspace>> pool;  // free wavefront workspaces, per device tagged
+    ~rt_scene() {
+        for (auto& d : dev)
+            if (d.blob) (void)hipFree(d.blob);
+        pool.clear();
+    }
+};
+
+namespace {
+
+void cp3(double* dst, const rt::host::D3& v) {
+    dst[0] = v.x;
+    dst[1] = v.y;
+    dst[2] = v.z;
+}
+
+void pack_scene(rt_scene* s) {
+    using namespace rt::host;
+    Packed& p = s->packed;
+    const Scene& sc = s->host;
+    for (const Mesh& m : sc.meshes) {
+        rt::DevMesh dm{};
+        dm.node_base = (int32_t)p.meta.size();
+        dm.n_nodes = (int32_t)m.octree.size();
+        dm.ref_base = (int32_t)p.refs.size();
+        dm.n_refs = (int32_t)m.octree.refs.size();
+        dm.tri_base = (int32_t)p.tris.size();
+        dm.n_tris = (int32_t)m.num_triangles();
+        const Box& rb = m.octree.root;
+        double rbox[6] = {rb.min.x, rb.min.y, rb.min.z, rb.max.x, rb.max.y, rb.max.z};
+        std::memcpy(dm.root_box, rbox, sizeof rbox);
+        // root octant centres, with the same arithmetic as BoundingBox::octant(i).center()
+        D3 c{(rb.min.x + rb.max.x) / 2.0, (rb.min.y + rb.max.y) / 2.0, (rb.min.z + rb.max.z) / 2.0};
+        for (int i = 0; i < 8; ++i) {
+            D3 lo{(i & 4) ? c.x : rb.min.x, (i & 2) ? c.y : rb.min.y, (i & 1) ? c.z : rb.min.z};
+            D3 hi{(i & 4) ? rb.max.x : c.x, (i & 2) ? rb.max.y : c.y, (i & 1) ? rb.max.z : c.z};
+            dm.oct_center[i][0] = (lo.x + hi.x) / 2.0;
+            dm.oct_center[i][1] = (lo.y + hi.y) / 2.0;
+            dm.oct_center[i][2] = (lo.z + hi.z) / 2.0;
+        }
+        dm.surface_area = m.surface_area;
+        double cum = 0.0;
+        for (size_t t = 0; t < m.num_triangles(); ++t) {
+            D3 a = m.vertices[m.indices[3 * t]], b = m.vertices[m.indices[3 * t + 1]], cc = m.vertices[m.indices[3 * t + 2]];
+            rt::DevTri dt{};
+            D3 ab{b.x - a.x, b.y - a.y, b.z - a.z}, ac{cc.x - a.x, cc.y - a.y, cc.z - a.z};
+            // Triangle::normal: (c - a).cross(b - a).norm()
+            D3 cr{ac.y * ab.z - ac.z * ab.y, ac.z * ab.x - ac.x * ab.z, ac.x * ab.y - ac.y * ab.x};
+            double mg = std::sqrt(cr.x * cr.x + cr.y * cr.y + cr.z * cr.z);
+            D3 n{cr.x / mg, cr.y / mg, cr.z / mg};
+            cp3(dt.a, a);
+            cp3(dt.ab, ab);
+            cp3(dt.ac, ac);
+            cp3(dt.n, n);
+            p.tris.push_back(dt);
+            cum += t < m.areas.size() ? m.areas[t] : 0.0;
+            p.cum_area.push_back(cum);
+        }
+        dm.total_weight = cum;
+        const Octree& oc = m.octree;
+        for (size_t i = 0; i < oc.size(); ++i) {
+            rt::NodeMeta nm{};
+            nm.leaf_off = oc.kind[i] ? oc.leaf_off[i] + dm.ref_base : -1;
+            nm.leaf_cnt = oc.leaf_cnt[i];
+            nm.parent = oc.parent[i] >= 0 ? oc.parent[i] + dm.node_base : -1;
+            nm.slot = oc.slot[i];
+            p.meta.push_back(nm);
+            for (int k = 0; k < 8; ++k) {
+                int32_t c8 = oc.child[8 * i + k];
+                p.child.push_back(c8 >= 0 ? c8 + dm.node_base : -1);
+            }
+            const Box& b = oc.box[i];
+            double bb[6] = {b.min.x, b.min.y, b.min.z, b.max.x, b.max.y, b.max.z};
+            p.box.insert(p.box.end(), bb, bb + 6);
+        }
+        for (int32_t r : oc.refs) p.refs.push_back(r + dm.tri_base);
+        p.meshes.push_back(dm);
+    }
+    for (const Object& o : sc.objects) {
+        rt::DevObject d{};
+        d.geom = o.geom;
+        d.brdf = o.brdf;
+        d.mesh = o.mesh;
+        d.ph_power = o.ph_power;
+        cp3(d.emitted, o.emitted);
+        cp3(d.k, o.k);
+        cp3(d.pos, o.pos);
+        d.r = o.r;
+        cp3(d.n, o.n);
+        d.ph_kd = o.ph_kd;
+        d.ph_ks = o.ph_ks;
+        cp3(d.color_d, o.color_d);
+        cp3(d.color_s, o.color_s);
+        d.emissive = (o.emitted.x != 0.0 || o.emitted.y != 0.0 || o.emitted.z != 0.0) ? 1 : 0;
+        p.objects.push_back(d);
+    }
+}
+
+template <class T>
+void put(std::vector<char>& blob, size_t* off, const std::vector<T>& v) {
+    *off = align_up(blob.size(), 256);
+    blob.resize(*off + v.size() * sizeof(T) + 16);
+    if (!v.empty()) std::memcpy(blob.data() + *off, v.data(), v.size() * sizeof(T));
+}
+
+int upload(rt_scene* s, int device, rt::DevScene* out) {
+    std::lock_guard<std::mutex> lk(s->mu);
+    if ((int)s->dev.size() <= device) s->dev.resize(device + 1);
+    DeviceCopy& dc = s->dev[device];
+    if (!dc.ready) {
+        const Packed& p = s->packed;
+        std::vector<char> blob;
+        size_t o_obj, o_mesh, o_meta, o_child, o_box, o_refs, o_tris, o_cum;
+        put(blob, &o_obj, p.objects);
+        put(blob, &o_mesh, p.meshes);
+        put(blob, &o_meta, p.meta);
+        put(blob, &o_child, p.child);
+        put(blob, &o_box, p.box);
+        put(blob, &o_refs, p.refs);
+        put(blob, &o_tris, p.tris);
+        put(blob, &o_cum, p.cum_area);
+        void* d = nullptr;
+        HIP_TRY(hipMalloc(&d, blob.size()));
+        hipError_t e = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(d);
+            return fail(RT_E_HIP, std::string("scene upload: ") + hipGetErrorString(e));
+        }
+        char* b = (char*)d;
+        rt::DevScene ds{};
+        ds.objects = (const rt::DevObject*)(b + o_obj);
+        ds.meshes = (const rt::DevMesh*)(b + o_mesh);
+        ds.node_meta = (const rt::NodeMeta*)(b + o_meta);
+        ds.node_child = (const int32_t*)(b + o_child);
+        ds.node_box = (const double*)(b + o_box);
+        ds.tri_ref = (const int32_t*)(b + o_refs);
+        ds.tris = (const rt::DevTri*)(b + o_tris);
+        ds.tri_cum_area = (const double*)(b + o_cum);
+        ds.n_objects = (int32_t)p.objects.size();
+        ds.light = s->host.light;
+        ds.n_meshes = (int32_t)p.meshes.size();
+        cp3(ds.cam_pos, s->host.cam_pos);
+        cp3(ds.cam_dir, s->host.cam_dir);
+        dc.blob = d;
+        dc.ds = ds;
+        dc.ready = true;
+    }
+    *out = dc.ds;
+    return RT_OK;
+}
+
+int check_params(const rt_render_params* p) {
+    if (!p) return fail(RT_E_INVAL, "null params");
+    if (p->width <= 0 || p->height <= 0) return fail(RT_E_INVAL, "width/height must be positive");
+    if (p->tile_w < 0 || p->tile_h < 0 || p->x0 < 0 || p->y0 < 0 || p->x0 + p->tile_w > p->width ||
+        p->y0 + p->tile_h > p->height)
+        return fail(RT_E_INVAL, "tile outside the image");
+    if ((int64_t)p->width * p->height > (int64_t)UINT32_MAX) return fail(RT_E_INVAL, "image too large for 32-bit pixel ids");
+    return RT_OK;
+}
+
+std::unique_ptr<rt::Workspace> take_workspace(rt_scene* s, int device) {
+    std::lock_guard<std::mutex> lk(s->mu);
+    for (size_t i = 0; i < s->pool.size(); ++i) {
+        if (s->pool[i]->device == device) {
+            std::unique_ptr<rt::Workspace> w = std::move(s->pool[i]);
+            s->pool.erase(s->pool.begin() + i);
+            return w;
+        }
+    }
+    auto w = std::make_unique<rt::Workspace>();
+    w->device = device;
+    return w;
+}
+void give_workspace(rt_scene* s, std::unique_ptr<rt::Workspace> w) {
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->pool.push_back(std::move(w));
+}
+
+// Enqueue one render on `st` (device buffers). `cancel` is polled by the wavefront driver.
+int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, double* d_sub, hipStream_t st,
+                   const volatile int32_t* cancel, rt_render_stats* stats) {
+    int rc = check_params(p);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipSetDevice(p->device));
+    rt::DevScene ds;
+    rc = upload(s, p->device, &ds);
+    if (rc != RT_OK) return rc;
+    rt::RenderArgs a{};
+    a.width = p->width;
+    a.height = p->height;
+    a.x0 = p->x0;
+    a.y0 = p->y0;
+    a.tw = p->tile_w;
+    a.th = p->tile_h;
+    a.n_samples = p->spp > 0 ? p->spp / 4 : 0;  // server.rs:332 (i32 division)
+    a.mis = (p->flags & RT_FLAG_MIS) ? 1 : 0;
+    a.seed = p->seed;
+    rt::host::camera_frame(s->host, p->width, p->height, a.cx, a.cy);
+    a.inv_n = a.n_samples > 0 ? 1. / (double)a.n_samples : 0.0;
+    a.sub_out = d_sub;
+    a.rgb_out = d_rgb;
+    if (p->flags & RT_FLAG_FP32) return fail(RT_E_INVAL, "RT_FLAG_FP32 is not available in this build");
+    std::unique_ptr<rt::Workspace> ws = take_workspace(s, p->device);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (stats) {
+        std::memset(stats, 0, sizeof *stats);
+        HIP_TRY(hipEventCreate(&e0));
+        HIP_TRY(hipEventCreate(&e1));
+        HIP_TRY(hipEventRecord(e0, st));
+    }
+    int out = RT_OK;
+    std::string err;
+    if (p->flags & RT_FLAG_MEGAKERNEL) {
+        hipError_t e = ws->ensure_counters();
+        if (e == hipSuccess && stats) e = hipMemsetAsync(ws->counters, 0, 8 * sizeof(unsigned long long), st);
+        if (e == hipSuccess) {
+            a.counters = stats ? ws->counters : nullptr;
+            e = rt::launch_megakernel_f64(ds, a, st);
+        }
+        if (e != hipSuccess) { out = RT_E_HIP; err = std::string("megakernel: ") + hipGetErrorString(e); }
+    } else {
+        out = rt::wavefront_render_f64(ds, a, *ws, st, cancel, stats, &err);
+    }
+    if (stats && out >= 0) {
+        hipError_t e = hipEventRecord(e1, st);
+        if (e == hipSuccess) e = hipEventSynchronize(e1);
+        float ms = 0.f;
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+        if (e == hipSuccess && (p->flags & RT_FLAG_MEGAKERNEL)) {
+            unsigned long long cnt[1] = {0};
+            e = hipMemcpy(cnt, ws->counters, sizeof cnt, hipMemcpyDeviceToHost);
+            stats->vertices = (int64_t)cnt[0];
+            stats->kernel_ms[0] = ms;
+            stats->kernel_launches[0] = 1;
+        }
+        if (e != hipSuccess && out == RT_OK) { out = RT_E_HIP; err = std::string("stats: ") + hipGetErrorString(e); }
+        stats->device_ms = ms;
+        stats->samples = (int64_t)p->tile_w * p->tile_h * 4 * (int64_t)a.n_samples;
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    give_workspace(s, std::move(ws));
+    if (out < 0) return fail(out, err);
+    return out;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+static int finish_scene(rt::host::Scene&& sc, rt_scene** out) {
+    auto s = std::make_unique<rt_scene>();
+    s->host = std::move(sc);
+    pack_scene(s.get());
+    *out = s.release();
+    return RT_OK;
+}
+
+int rt_scene_load_toml(const char* toml_path, const char* assets_dir, rt_scene** out) {
+    if (!toml_path || !out) return fail(RT_E_INVAL, "null argument");
+    *out = nullptr;
+    std::string path(toml_path), assets;
+    if (assets_dir) assets = assets_dir;
+    else {
+        size_t sl = path.find_last_of('/');
+        assets = (sl == std::string::npos ? std::string(".") : path.substr(0, sl)) + "/assets";
+    }
+    rt::host::Scene sc;
+    std::string err;
+    int rc = rt::host::load_scene_toml(path, assets, &sc, &err);
+    if (rc != RT_OK) return fail(rc, err);
+    return finish_scene(std::move(sc), out);
+}
+
+int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
+    if (!out) return fail(RT_E_INVAL, "null argument");
+    *out = nullptr;
+    rt::host::Scene sc;
+    std::string err;
+    int rc = rt::host::scene_from_desc(desc, &sc, &err);
+    if (rc != RT_OK) return fail(rc, err);
+    return finish_scene(std::move(sc), out);
+}
+
+void rt_scene_destroy(rt_scene* s) { delete s; }
+
+int rt_scene_info(const rt_scene* s, int64_t info[16]) {
+    if (!s || !info) return fail(RT_E_INVAL, "null argument");
+    std::memset(info, 0, 16 * sizeof(int64_t));
+    info[0] = (int64_t)s->host.objects.size();
+    info[1] = s->host.light;
+    info[2] = (int64_t)s->host.meshes.size();
+    for (const auto& m : s->host.meshes) {
+        info[3] += (int64_t)m.octree.size();
+        info[4] += m.octree.parents;
+        info[5] += m.octree.leaves;
+        info[6] += (int64_t)m.octree.refs.size();
+        info[7] += (int64_t)m.num_triangles();
+        info[8] += (int64_t)m.vertices.size();
+        if (m.octree.max_leaf > info[9]) info[9] = m.octree.max_leaf;
+        if (m.octree.max_depth > info[10]) info[10] = m.octree.max_depth;
+    }
+    return RT_OK;
+}
+
+int rt_scene_mesh(const rt_scene* s, int32_t object, int64_t counts[4], double bbox[6], double* surface_area,
+                  double* vertices, uint32_t* indices, int32_t* kind, int32_t* child, int32_t* leaf_off,
+                  int32_t* leaf_cnt, int32_t* refs) {
+    if (!s || object < 0 || (size_t)object >= s->host.objects.size()) return fail(RT_E_INVAL, "bad object index");
+    const auto& o = s->host.objects[object];
+    if (o.geom != RT_GEOM_MESH) return fail(RT_E_INVAL, "object is not a mesh");
+    const auto& m = s->host.meshes[o.mesh];
+    const auto& oc = m.octree;
+    if (counts) {
+        counts[0] = (int64_t)oc.size();
+        counts[1] = (int64_t)oc.refs.size();
+        counts[2] = (int64_t)m.num_triangles();
+        counts[3] = (int64_t)m.vertices.size();
+    }
+    if (bbox) {
+        double b[6] = {m.bbox.min.x, m.bbox.min.y, m.bbox.min.z, m.bbox.max.x, m.bbox.max.y, m.bbox.max.z};
+        std::memcpy(bbox, b, sizeof b);
+    }
+    if (surface_area) *surface_area = m.surface_area;
+    if (vertices)
+        for (size_t i = 0; i < m.vertices.size(); ++i) {
+            vertices[3 * i] = m.vertices[i].x;
+            vertices[3 * i + 1] = m.vertices[i].y;
+            vertices[3 * i + 2] = m.vertices[i].z;
+        }
+    if (indices) std::memcpy(indices, m.indices.data(), m.indices.size() * sizeof(uint32_t));
+    for (size_t i = 0; i < oc.size(); ++i) {
+        if (kind) kind[i] = oc.kind[i];
+        if (child) std::memcpy(child + 8 * i, &oc.child[8 * i], 8 * sizeof(int32_t));
+        if (leaf_off) leaf_off[i] = oc.leaf_off[i];
+        if (leaf_cnt) leaf_cnt[i] = oc.leaf_cnt[i];
+    }
+    if (refs) std::memcpy(refs, oc.refs.data(), oc.refs.size() * sizeof(int32_t));
+    return RT_OK;
+}
+
+int rt_render_device(const rt_scene* scene, const rt_render_params* params, void* d_rgb, void* d_sub, void* stream,
+                     rt_render_stats* stats) {
+    if (!scene || !d_rgb) return fail(RT_E_INVAL, "null argument");
+    return render_enqueue(const_cast<rt_scene*>(scene), params, (uint8_t*)d_rgb, (double*)d_sub, (hipStream_t)stream,
+                          nullptr, stats);
+}
+
+int rt_render(const rt_scene* scene, const rt_render_params* p, uint8_t* rgb_out, double* sub_out,
+              const volatile int32_t* cancel, rt_render_stats* stats) {
+    if (!scene || !rgb_out) return fail(RT_E_INVAL, "null argument");
+    int rc = check_params(p);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipSetDevice(p->device));
+    size_t npix = (size_t)p->tile_w * p->tile_h;
+    if (npix == 0) return RT_OK;
+    uint8_t* d_rgb = nullptr;
+    double* d_sub = nullptr;
+    hipStream_t st = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    hipError_t e = hipMalloc(&d_rgb, npix * 3);
+    if (e == hipSuccess && sub_out) e = hipMalloc(&d_sub, npix * 12 * sizeof(double));
+    if (e != hipSuccess) {
+        if (d_rgb) (void)hipFree(d_rgb);
+        (void)hipStreamDestroy(st);
+        return fail(RT_E_OOM, std::string("output buffers: ") + hipGetErrorString(e));
+    }
+    rt_render_stats local;
+    rc = render_enqueue(const_cast<rt_scene*>(scene), p, d_rgb, d_sub, st, cancel, stats ? stats : &local);
+    std::string err = g_err;
+    if (rc == RT_OK) {
+        e = hipMemcpyAsync(rgb_out, d_rgb, npix * 3, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess && sub_out) e = hipMemcpyAsync(sub_out, d_sub, npix * 12 * sizeof(double), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) { rc = RT_E_HIP; err = std::string("readback: ") + hipGetErrorString(e); }
+    } else {
+        (void)hipStreamSynchronize(st);
+    }
+    (void)hipFree(d_rgb);
+    if (d_sub) (void)hipFree(d_sub);
+    (void)hipStreamDestroy(st);
+    if (rc < 0) return fail(rc, err);
+    return rc;
+}
+
+int rt_trace_rays(const rt_scene* scene, int32_t device, int64_t n, const double* origins, const double* dirs, double* t,
+                  int32_t* object, double* pos, double* normal) {
+    if (!scene || n < 0 || (n && (!origins || !dirs || !t || !object))) return fail(RT_E_INVAL, "null argument");
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(device));
+    rt::DevScene ds;
+    int rc = upload(const_cast<rt_scene*>(scene), device, &ds);
+    if (rc != RT_OK) return rc;
+    size_t v3 = (size_t)n * 3 * sizeof(double);
+    char* buf = nullptr;
+    size_t total = 4 * v3 + (size_t)n * sizeof(double) + (size_t)n * sizeof(int32_t);
+    HIP_TRY(hipMalloc((void**)&buf, total));
+    double* d_o = (double*)buf;
+    double* d_d = (double*)(buf + v3);
+    double* d_pos = (double*)(buf + 2 * v3);
+    double* d_n = (double*)(buf + 3 * v3);
+    double* d_t = (double*)(buf + 4 * v3);
+    int32_t* d_id = (int32_t*)(buf + 4 * v3 + (size_t)n * sizeof(double));
+    hipError_t e = hipMemcpy(d_o, origins, v3, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_d, dirs, v3, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rt::launch_trace_f64(ds, (long)n, d_o, d_d, d_t, d_id, d_pos, d_n, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(t, d_t, (size_t)n * sizeof(double), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(object, d_id, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && pos) e = hipMemcpy(pos, d_pos, v3, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && normal) e = hipMemcpy(normal, d_n, v3, hipMemcpyDeviceToHost);
+    (void)hipFree(buf);
+    if (e != hipSuccess) return fail(RT_E_HIP, std::string("rt_trace_rays: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+}  // extern "C"
