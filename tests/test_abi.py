@@ -1,0 +1,45 @@
+"""The C ABI library loads and exports every entry point include/rt_ffi.h declares, and the ctypes
+mirror's struct layouts match the header (compiled with gcc). CPU only: no compute calls."""
+import ctypes
+import os
+import re
+import subprocess
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "rt_ffi.h")
+
+
+def declared():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(rt_[a-z_0-9]+)\s*\(", text, re.M)))
+
+
+def test_exports_every_declared_symbol(rt):
+    names = declared()
+    assert len(names) >= 11
+    for n in names:
+        assert hasattr(rt.lib, n), f"missing export {n}"
+    assert rt.lib.rt_abi_version() == 1
+
+
+def test_struct_layout_matches_header(rt, tmp_path):
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "rt_ffi.h"\nint main(void){'
+                   'printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(rt_render_params), sizeof(rt_render_stats),'
+                   'sizeof(rt_object_desc), sizeof(rt_mesh_desc), sizeof(rt_scene_desc),'
+                   'offsetof(rt_render_params, seed), offsetof(rt_object_desc, mesh));return 0;}')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    want = [ctypes.sizeof(rt.RenderParams), ctypes.sizeof(rt.RenderStats), ctypes.sizeof(rt.ObjectDesc),
+            ctypes.sizeof(rt.MeshDesc), ctypes.sizeof(rt.SceneDesc), rt.RenderParams.seed.offset,
+            rt.ObjectDesc.mesh.offset]
+    assert got == want
+
+
+def test_errors_are_codes_not_crashes(rt):
+    h = ctypes.c_void_p()
+    assert rt.lib.rt_scene_load_toml(b"/nonexistent.toml", None, ctypes.byref(h)) == -4
+    assert b"nonexistent" in rt.lib.rt_last_error()
+    assert rt.lib.rt_render(None, None, None, None, None, None) == -1

@@ -1,0 +1,129 @@
+"""Product host prep (C++ in librtamd.so, no GPU calls) against the oracle's restatement (CPU only):
+scene loading (SceneSpec::to_scene, scene.rs:357-441), OBJ loading, transforms and the octree
+(geometry.rs:1145-1216) must be bit-identical; malformed inputs must fail with an error code,
+never crash (the reference panics)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import scene_path
+
+
+@pytest.mark.parametrize("name", ["cornell_box", "cubes", "flying_unicorn"])
+def test_scene_prep_matches_oracle(name, rt, oracle_scenes):
+    s = rt.Scene.from_toml(scene_path(name))
+    o = oracle_scenes[name]
+    info = s.info()
+    assert info["objects"] == len(o.objects) and info["light"] == o.light == 8
+    for i, kind in enumerate(o.objects):
+        if kind not in ("mesh", "cube", "prism"):
+            continue
+        m = s.mesh(i)
+        st = o.mesh_stats(i)
+        kind_o, child_o, off_o, cnt_o, refs_o = o.mesh_octree(i)
+        verts_o, idx_o = o.mesh_vertices(i)
+        assert np.array_equal(m["vertices"], verts_o)  # bitwise: transforms replicated exactly
+        assert np.array_equal(m["indices"].astype(np.int64), idx_o.astype(np.int64))
+        assert np.array_equal(m["bbox"], st["bbox"]) and m["surface_area"] == st["surface_area"]
+        assert np.array_equal(m["kind"], kind_o) and np.array_equal(m["child"], child_o)
+        assert np.array_equal(m["leaf_cnt"], cnt_o) and np.array_equal(m["refs"], refs_o)
+
+
+def test_unicorn_info(rt):
+    info = rt.Scene.from_toml(scene_path("flying_unicorn")).info()
+    assert (info["nodes"], info["parents"], info["leaves"], info["refs"]) == (47183, 9540, 37643, 187766)
+    assert info["max_leaf"] == 12 and info["max_depth"] == 10
+
+
+def _write(tmp_path, text, name="s.toml"):
+    p = tmp_path / name
+    p.write_text(text)
+    return str(p)
+
+
+GOOD = """
+[camera]
+pos = [50, 52, 295.6]   # integers are accepted for f64 fields (serde)
+dir = [0.0, -0.042612, -1.0]
+[[objects]]
+brdf = { type = "diffuse", kd = [0.75, 0.25, 0.25] }
+geometry = { type = "plane", pos = [1.0, 0.0, 0.0], n = [-1.0, 0.0, 0.0] }
+[[objects]]
+emitted = [50.0, 50.0, 50.0]
+brdf = { type = "diffuse", kd = [0.0, 0.0, 0.0] }
+geometry = { type = "sphere", pos = [50.0, 70.0, 100.0], r = 4.0 }
+transforms = [
+    { translate = [1, 0, 0] },
+    { scale = 2.0 },
+]
+"""
+
+
+def test_toml_subset_parses(rt, tmp_path):
+    s = rt.Scene.from_toml(_write(tmp_path, GOOD))
+    assert s.info()["objects"] == 2 and s.info()["light"] == 1
+
+
+@pytest.mark.parametrize("text,needle", [
+    ("[camera]\npos=[0,0,0]\n", "dir"),
+    (GOOD.replace('"diffuse", kd = [0.75', '"velvet", kd = [0.75'), "velvet"),
+    (GOOD.replace("[0.0, -0.042612, -1.0]", "[0.0, -1.0]"), "3"),
+    (GOOD.replace("{ scale = 2.0 }", "{ shear = 2.0 }"), "shear"),
+    (GOOD.replace("emitted = [50.0, 50.0, 50.0]", "emitted = [0.0, 0.0, 0.0]"), "emitting"),
+    (GOOD.replace('type = "sphere", pos', 'type = "plane", n = [0,1,0], pos').replace(", r = 4.0", ""), "plane"),
+    ("[camera\npos = [1,2,3]\n", "line"),
+    (GOOD + "\n[camera]\n", "twice"),
+])
+def test_toml_errors(rt, tmp_path, text, needle):
+    with pytest.raises(rt.RtError) as e:
+        rt.Scene.from_toml(_write(tmp_path, text))
+    assert needle in str(e.value)
+
+
+def test_obj_errors(rt, tmp_path):
+    (tmp_path / "assets").mkdir()
+    base = GOOD + '\n[[objects]]\nbrdf = { type = "diffuse", kd = [1,1,1] }\ngeometry = { type = "mesh", path = "m.obj" }\n'
+    p = _write(tmp_path, base)
+    with pytest.raises(rt.RtError) as e:
+        rt.Scene.from_toml(p)
+    assert e.value.code == -4  # RT_E_IO: missing asset
+    for bad in ["v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 4\n", "v 0 0 x\n", "v 0 0 0\nf 1//1 1 1\n", "f 1 2\n"]:
+        (tmp_path / "assets" / "m.obj").write_text(bad)
+        with pytest.raises(rt.RtError):
+            rt.Scene.from_toml(p)
+    (tmp_path / "assets" / "m.obj").write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\nvn 0 0 1\nf 1/1/1 +2/2/2 3\n")
+    s = rt.Scene.from_toml(p)
+    m = s.mesh(2)
+    assert m["indices"].tolist() == [[0, 1, 2]]
+
+
+def test_scene_create_from_desc_matches_toml(rt):
+    """rt_scene_create (the host-keeps-its-loader boundary) builds the same octree as the TOML path."""
+    t = rt.Scene.from_toml(scene_path("flying_unicorn"))
+    m = t.mesh(6)
+    objs = []
+    import tomli
+    spec = tomli.load(open(scene_path("flying_unicorn"), "rb"))
+    for o in spec["objects"]:
+        g, b = o["geometry"], o["brdf"]
+        d = dict(emitted=o.get("emitted", [0, 0, 0]), brdf_kind={"diffuse": 0, "specular": 1}[b["type"]],
+                 k=b.get("kd", b.get("ks")))
+        if g["type"] == "plane":
+            d.update(geom_kind=1, pos=g["pos"], n=g["n"])
+        elif g["type"] == "sphere":
+            d.update(geom_kind=0, pos=g["pos"], r=g["r"])
+        else:
+            d.update(geom_kind=2, mesh=0)
+        objs.append(d)
+    mesh = dict(vertices=m["vertices"], indices=m["indices"], bbox_min=m["bbox"][:3], bbox_max=m["bbox"][3:],
+                surface_area=m["surface_area"])
+    s = rt.Scene.from_desc(spec["camera"]["pos"], spec["camera"]["dir"], objs, [mesh])
+    m2 = s.mesh(6)
+    assert np.array_equal(m2["child"], m["child"]) and np.array_equal(m2["refs"], m["refs"])
+    assert s.info() == t.info()
+
+
+def test_bad_desc_rejected(rt):
+    with pytest.raises(rt.RtError):
+        rt.Scene.from_desc([0, 0, 0], [0, 0, -1], [dict(geom_kind=2, mesh=3, emitted=[1, 1, 1])], [])

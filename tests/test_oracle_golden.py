@@ -1,0 +1,80 @@
+"""Pins the CPU oracle before it is trusted as the checker (CPU only).
+
+  * geometry.rs:1115-1131 `test_octants` — the reference's only unit test, restated;
+  * Random123 Philox4x32-10 known-answer vectors (the RNG spec's first stage);
+  * octree shape of flying_unicorn (47,183 nodes / 9,540 parents / 37,643 leaves /
+    187,766 refs) and the transformed bbox;
+  * the reference's own example render examples/cornell_box.png (64 spp) — statistical golden:
+    image mean within 0.5 u8, 30x30-block means within 5 u8 (mean |diff| <= 1.2);
+  * path statistics SURVEY §8(d) relies on (15.0 vertices, 29.5 casts per sample).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+
+def test_octants_known_answer(oracle):
+    o = oracle.octants([-1, -1, -1], [1, 1, 1])
+    expect = [([-1, -1, -1], [0, 0, 0]), ([-1, -1, 0], [0, 0, 1]), ([-1, 0, -1], [0, 1, 0]),
+              ([-1, 0, 0], [0, 1, 1]), ([0, -1, -1], [1, 0, 0]), ([0, -1, 0], [1, 0, 1]),
+              ([0, 0, -1], [1, 1, 0]), ([0, 0, 0], [1, 1, 1])]
+    assert np.array_equal(o, np.array(expect, dtype=float))
+
+
+def test_philox_known_answers(oracle):
+    # Random123 kat_vectors, philox4x32_10
+    assert oracle.philox([0, 0, 0, 0], [0, 0]) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    assert oracle.philox([0xFFFFFFFF] * 4, [0xFFFFFFFF] * 2) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+    assert oracle.philox([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], [0xA4093822, 0x299F31D0]) == \
+        [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_draws_are_uniform_and_keyed(oracle):
+    a = np.array([oracle.draws(7, p, s, 3, 1, 5) for p in range(200) for s in range(20)])
+    assert a.min() >= 0.0 and a.max() < 1.0
+    assert abs(a.mean() - 0.5) < 0.01 and abs(a.var() - 1 / 12) < 0.005
+    assert not np.array_equal(oracle.draws(7, 1, 2, 3, 0), oracle.draws(7, 1, 2, 3, 1))
+    assert np.array_equal(oracle.draws(7, 1, 2, 3, 0), oracle.draws(7, 1, 2, 3, 0))
+
+
+def test_unicorn_octree_shape(oracle_scenes):
+    st = oracle_scenes["flying_unicorn"].mesh_stats(6)
+    assert (st["nodes"], st["parents"], st["leaves"], st["refs"]) == (47183, 9540, 37643, 187766)
+    assert st["n_tris"] == 37380 and st["n_verts"] == 18728 and st["max_leaf"] == 12
+    assert np.allclose(st["bbox"], [11.657, -2.801, 56.176, 52.060, 59.347, 91.408], atol=1e-3)
+
+
+def test_cubes_octree_shape(oracle_scenes):
+    for obj in (6, 7):
+        st = oracle_scenes["cubes"].mesh_stats(obj)
+        assert (st["nodes"], st["parents"], st["leaves"]) == (9, 1, 8)
+
+
+@pytest.mark.slow
+def test_cornell_example_render(oracle_scenes):
+    g = json.load(open(os.path.join(REPO, "tests", "golden", "cornell_box_example.json")))
+    rgb, _, st = oracle_scenes["cornell_box"].render(300, 225, 64, 0x5EED, want_sub=False)
+    mean = rgb.reshape(-1, 3).mean(0)
+    assert np.all(np.abs(mean - np.array(g["image_mean"])) < 0.5), mean
+    blocks = rgb.astype(float).reshape(15, 15, 20, 15, 3).mean(axis=(1, 3))
+    d = np.abs(blocks - np.array(g["block_means"]))
+    assert d.max() < 5.0 and d.mean() < 1.2, (d.max(), d.mean())
+    n = 300 * 225 * 64
+    assert 14.8 < st["vertices"] / n < 15.2  # V = 15.0
+    assert 29.2 < st["casts"] / n < 29.9     # 29.5 trace_ray calls per sample
+
+
+def test_spp_below_four_is_black(oracle_scenes):
+    rgb, sub, st = oracle_scenes["cornell_box"].render(40, 30, 3, 1)
+    assert not rgb.any() and not sub.any() and st["vertices"] == 0
+
+
+def test_oracle_tile_invariance(oracle_scenes):
+    s = oracle_scenes["cubes"]
+    full, sub, _ = s.render(40, 30, 4, 9)
+    t, st_sub, _ = s.render(40, 30, 4, 9, tile=(7, 5, 20, 11))
+    assert np.array_equal(t, full[5:16, 7:27]) and np.array_equal(st_sub, sub[5:16, 7:27])
