@@ -65,17 +65,18 @@ RT_DEV void begin_sample(const DevScene& sc, const RenderArgs& a, const SubPixel
 // Shades the hit `hr` of ps.ray. Returns true when the path continues (ps.ray is the next ray to
 // trace), false when this sample's radiance ps.L is final. The shadow ray of next-event estimation
 // is traced inline.
+template <class C>
 RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, const SubPixel& sp, int smp, PathState& ps,
                          const HitRec& hr) {
     if (hr.obj < 0) return false;  // no hit: R = 0 (scene.rs:157, :175, :233)
     const DevObject& obj = sc.objects[hr.obj];
     V3 x, nrm;
-    surface(sc, ps.ray, hr, &x, &nrm);
+    surface<C>(sc, ps.ray, hr, &x, &nrm);
     if (ps.kind == K_CAMERA) {
         ps.L = ld3(obj.emitted);
     } else if (ps.kind == K_SPEC) {
         ps.L = ps.L + mult(ps.bemit, ld3(obj.emitted));
-    } else if (a.mis && hr.obj == sc.light && ps.pdf_prev > 0.0) {
+    } else if (C::mis && hr.obj == sc.light && ps.pdf_prev > 0.0) {
         // MIS, BSDF strategy: emitted radiance with the balance-heuristic weight
         double cosl = dot(nrm, -ps.ray.d);
         double pdf_l = light_pdf_area(sc) * (hr.t * hr.t) / cosl;
@@ -92,25 +93,25 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, const SubPixel
         if (!(d.v[2] < p)) return false;
         V3 i;
         double pdf;
-        brdf_sample(obj, nrm, ps.o, d, &i, &pdf);
-        V3 f = brdf_eval(obj, nrm, ps.o, i);
+        brdf_sample<C>(obj, nrm, ps.o, d, &i, &pdf);
+        V3 f = brdf_eval<C>(obj, nrm, ps.o, i);
         ps.bemit = ps.beta;
         ps.beta = mult(ps.beta, f) * dot(nrm, i) / (pdf * p);
         ps.ray = Ray{x, i};
         ps.kind = K_SPEC;
         return true;
     }
-    draw_vertex(rng, d, obj.brdf == BRDF_PHONG ? 6 : 5);
-    const bool use_mis = a.mis && obj.brdf == BRDF_DIFFUSE;
+    draw_vertex(rng, d, (C::phong && obj.brdf == BRDF_PHONG) ? 6 : 5);
+    const bool use_mis = C::mis && obj.brdf == BRDF_DIFFUSE;
     // next-event estimation (scene.rs:217-229)
     V3 y, ny;
     double pdfA;
-    light_sample(sc, d, &y, &ny, &pdfA);
+    light_sample<C>(sc, d, &y, &ny, &pdfA);
     V3 i = norm(y - x);
     double r_sqr = dot(y - x, y - x);
-    V3 lef = mult(ld3(sc.objects[sc.light].emitted), brdf_eval(obj, nrm, ps.o, i));
+    V3 lef = mult(ld3(sc.objects[sc.light].emitted), brdf_eval<C>(obj, nrm, ps.o, i));
     if (!is_zero(lef)) {  // a zero Le*f makes the term exactly 0: skip the shadow ray
-        double vis = visible(sc, x, y) ? 1. : 0.;
+        double vis = visible<C>(sc, x, y) ? 1. : 0.;
         V3 c;
         if (!use_mis) {
             c = lef * vis * dot(nrm, i) * dot(ny, -i) / (r_sqr * pdfA);
@@ -127,8 +128,8 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, const SubPixel
     if (!(d.v[2] < p)) return false;
     V3 wi;
     double pdf;
-    brdf_sample(obj, nrm, ps.o, d, &wi, &pdf);
-    V3 f = brdf_eval(obj, nrm, ps.o, wi);
+    brdf_sample<C>(obj, nrm, ps.o, d, &wi, &pdf);
+    V3 f = brdf_eval<C>(obj, nrm, ps.o, wi);
     ps.beta = mult(ps.beta, f) * dot(nrm, wi) / (pdf * p);
     ps.ray = Ray{x, wi};
     ps.kind = K_DIFF;

@@ -31,7 +31,24 @@ RT_DEV V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 RT_DEV V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
 RT_DEV V3 operator*(V3 a, double s) { return v3(a.x * s, a.y * s, a.z * s); }
 RT_DEV V3 operator*(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
-RT_DEV V3 operator/(V3 a, double s) { return v3(a.x / s, a.y / s, a.z / s); }
+// ---- correctly rounded division with a shared divisor ----
+// q = RN(a / b) from y = RN(1 / b): q0 = RN(a y), r = a - b q0 (exact, FMA), q = RN(q0 + r y)
+// (Markstein's theorem; valid without overflow/underflow). Used only when |b| is in
+// [2^-900, 2^900]; otherwise, and for NaN/inf, the plain IEEE division is taken. r == 0 means q0
+// is the exact quotient (keeps the sign of a zero quotient). Bit-identical to a / b.
+RT_DEV bool rcp_safe(double b) { return fabs(b) >= 0x1p-900 && fabs(b) <= 0x1p900; }
+RT_DEV double qdiv(double a, double b, double y) {
+    double q0 = a * y;
+    double r = fma(-b, q0, a);
+    return r == 0.0 ? q0 : fma(r, y, q0);
+}
+RT_DEV V3 operator/(V3 a, double s) {
+    if (rcp_safe(s)) {
+        double y = 1.0 / s;
+        return v3(qdiv(a.x, s, y), qdiv(a.y, s, y), qdiv(a.z, s, y));
+    }
+    return v3(a.x / s, a.y / s, a.z / s);
+}
 RT_DEV double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 RT_DEV V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
 RT_DEV V3 mult(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
@@ -63,6 +80,26 @@ struct Ray {
     V3 o, d;
 };
 RT_DEV V3 eval(const Ray& r, double t) { return r.o + t * r.d; }
+
+// Per-ray reciprocals of the direction for the divisions x / d.{x,y,z} (box faces, axis planes).
+// A component outside the safe range (0, tiny, huge, NaN) falls back to the IEEE division.
+struct RayInv {
+    double rx, ry, rz;
+    bool fx, fy, fz;  // fast (Markstein) path usable
+};
+RT_DEV RayInv make_inv(const V3& d) {
+    RayInv v;
+    v.fx = rcp_safe(d.x);
+    v.fy = rcp_safe(d.y);
+    v.fz = rcp_safe(d.z);
+    v.rx = v.fx ? 1.0 / d.x : 0.0;
+    v.ry = v.fy ? 1.0 / d.y : 0.0;
+    v.rz = v.fz ? 1.0 / d.z : 0.0;
+    return v;
+}
+RT_DEV double div_x(double a, const Ray& r, const RayInv& v) { return v.fx ? qdiv(a, r.d.x, v.rx) : a / r.d.x; }
+RT_DEV double div_y(double a, const Ray& r, const RayInv& v) { return v.fy ? qdiv(a, r.d.y, v.ry) : a / r.d.y; }
+RT_DEV double div_z(double a, const Ray& r, const RayInv& v) { return v.fz ? qdiv(a, r.d.z, v.rz) : a / r.d.z; }
 
 // ---------------------------------------------------------------- RNG
 struct Rng {
@@ -121,7 +158,19 @@ RT_DEV bool sphere_t(const DevObject& o, const Ray& ray, double* tout) {
     if (t > eps) { *tout = t; return true; }
     return false;
 }
-RT_DEV bool plane_t(const DevObject& o, const Ray& ray, double* tout) {
+RT_DEV bool plane_t(const DevObject& o, const Ray& ray, const RayInv& inv, double* tout) {
+    if (o.axis >= 0) {
+        // n = +-e_axis exactly: dot(pos - o, n) / dot(d, n) == (pos - o)_axis / d_axis bit for bit
+        // (the +-0 terms vanish and IEEE division is sign-symmetric); shares the ray reciprocal.
+        double dn, num, t;
+        if (o.axis == 0) { dn = ray.d.x; num = o.pos[0] - ray.o.x; }
+        else if (o.axis == 1) { dn = ray.d.y; num = o.pos[1] - ray.o.y; }
+        else { dn = ray.d.z; num = o.pos[2] - ray.o.z; }
+        if (fabs(dn) < 0.0001) return false;
+        t = o.axis == 0 ? div_x(num, ray, inv) : o.axis == 1 ? div_y(num, ray, inv) : div_z(num, ray, inv);
+        if (t >= 0.) { *tout = t; return true; }
+        return false;
+    }
     V3 n = ld3(o.n);
     double dn = dot(ray.d, n);
     if (fabs(dn) < 0.0001) return false;
@@ -137,32 +186,68 @@ RT_DEV bool tri_t(const DevTri& tr, const Ray& ray, double* tout) {
     V3 b = ray.o - ld3(tr.a);
     V3 nd = -ray.d;
     double det = det3(nd, ab, ac);
-    double t = det3(b, ab, ac) / det;
-    double u = det3(nd, b, ac) / det;
-    double v = det3(nd, ab, b) / det;
+    double tn = det3(b, ab, ac), un = det3(nd, b, ac), vn = det3(nd, ab, b);
+    double t, u, v;
+    if (rcp_safe(det)) {
+        double y = 1.0 / det;
+        t = qdiv(tn, det, y);
+        u = qdiv(un, det, y);
+        v = qdiv(vn, det, y);
+    } else {
+        t = tn / det;
+        u = un / det;
+        v = vn / det;
+    }
     if (u < 0. || u > 1. || v < 0. || u + v > 1.) return false;
     if (t > 0.0001) { *tout = t; return true; }
     return false;
 }
 // BoundingBox::intersect(..).is_some() (geometry.rs:977-1036): first face in order (-x,+x,-y,+y,-z,+z).
-RT_DEV bool box_hit(const double* bx, const Ray& r) {
+// The six divisions use the ray's reciprocals (bit-identical quotients, see qdiv).
+RT_DEV bool box_hit(const double* bx, const Ray& r, const RayInv& inv) {
     const double EPS = 0.0000001;
     const double mnx = bx[0], mny = bx[1], mnz = bx[2], mxx = bx[3], mxy = bx[4], mxz = bx[5];
     double t;
     V3 p;
-    t = (mnx - r.o.x) / r.d.x;
+    t = div_x(mnx - r.o.x, r, inv);
     if (t >= EPS) { p = eval(r, t); if (mny <= p.y && p.y <= mxy && mnz <= p.z && p.z <= mxz) return true; }
-    t = (mxx - r.o.x) / r.d.x;
+    t = div_x(mxx - r.o.x, r, inv);
     if (t >= EPS) { p = eval(r, t); if (mny <= p.y && p.y <= mxy && mnz <= p.z && p.z <= mxz) return true; }
-    t = (mny - r.o.y) / r.d.y;
+    t = div_y(mny - r.o.y, r, inv);
     if (t >= EPS) { p = eval(r, t); if (mnx <= p.x && p.x <= mxx && mnz <= p.z && p.z <= mxz) return true; }
-    t = (mxy - r.o.y) / r.d.y;
+    t = div_y(mxy - r.o.y, r, inv);
     if (t >= EPS) { p = eval(r, t); if (mnx <= p.x && p.x <= mxx && mnz <= p.z && p.z <= mxz) return true; }
-    t = (mnz - r.o.z) / r.d.z;
+    t = div_z(mnz - r.o.z, r, inv);
     if (t >= EPS) { p = eval(r, t); if (mnx <= p.x && p.x <= mxx && mny <= p.y && p.y <= mxy) return true; }
-    t = (mxz - r.o.z) / r.d.z;
+    t = div_z(mxz - r.o.z, r, inv);
     if (t >= EPS) { p = eval(r, t); if (mnx <= p.x && p.x <= mxx && mny <= p.y && p.y <= mxy) return true; }
     return false;
+}
+
+// Conservative cull: false only if the ray (t >= 0) passes farther than `pad` from the box, in
+// which case no box contained in it can pass box_hit (its face points would be within rounding,
+// ~1e-11, of the ray). Exactness argument in DESIGN.md §Octree.
+RT_DEV bool near_box(const double* bx, const Ray& r, const RayInv& inv, double pad) {
+    double t0 = 0.0, t1 = INFINITY;
+    const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+    const double rc[3] = {inv.rx, inv.ry, inv.rz};
+    const bool f[3] = {inv.fx, inv.fy, inv.fz};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        double lo = bx[k] - pad, hi = bx[3 + k] + pad;
+        if (!f[k]) {
+            if (fabs(d[k]) < 0x1p-900) {  // (nearly) parallel slab: origin must lie inside it
+                if (o[k] < lo || o[k] > hi) return false;
+                continue;
+            }
+            return true;  // NaN / huge: do not cull
+        }
+        double ta = (lo - o[k]) * rc[k], tb = (hi - o[k]) * rc[k];
+        double tn = fmin(ta, tb), tf = fmax(ta, tb);
+        t0 = fmax(t0, tn - 1e-9 * fabs(tn));
+        t1 = fmin(t1, tf + 1e-9 * fabs(tf));
+    }
+    return t0 <= t1;
 }
 
 // Leaf: nearest triangle, strict < (geometry.rs:1276-1293).
@@ -182,8 +267,9 @@ RT_DEV bool leaf_hit(const DevScene& sc, int off, int cnt, const Ray& ray, doubl
 // centre distances, insertion-sorted, strict >) is identical at every level, so the DFS resumes
 // from parent links + the child's slot rank instead of a stack. Same visiting order and the same
 // first-leaf-with-a-hit exit as the reference recursion; no per-lane stack memory.
-RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, double* t, int* prim) {
+RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double* t, int* prim) {
     if (m.n_nodes == 0) return false;
+    if (!near_box(m.root_box, ray, inv, m.cull_pad)) return false;
     const int root = m.node_base;
     NodeMeta rm = sc.node_meta[root];
     if (rm.leaf_off >= 0) return leaf_hit(sc, rm.leaf_off, rm.leaf_cnt, ray, t, prim);
@@ -218,7 +304,7 @@ RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, doubl
         for (; k < 8; ++k) {
             int oi = (order >> (4 * k)) & 0xF;
             int c = ch[oi];
-            if (c >= 0 && box_hit(sc.node_box + 6 * (size_t)c, ray)) { found = c; break; }
+            if (c >= 0 && box_hit(sc.node_box + 6 * (size_t)c, ray, inv)) { found = c; break; }
         }
         if (found >= 0) {
             NodeMeta fm = sc.node_meta[found];
@@ -238,11 +324,22 @@ RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, doubl
     }
 }
 
+// Kernel specialisation by scene features (chosen on the host per scene/flags): code paths a
+// scene cannot reach are not compiled into its kernels, which keeps register pressure down.
+template <int F>
+struct Cfg {
+    static constexpr bool mesh = (F & 1) != 0;   // scene has triangle meshes (octree traversal)
+    static constexpr bool phong = (F & 2) != 0;  // scene has a Phong BRDF
+    static constexpr bool mis = (F & 4) != 0;    // RT_FLAG_MIS
+};
+
 // One object's Geometry::intersect, reporting t (and the triangle for meshes).
-RT_DEV bool object_t(const DevScene& sc, const DevObject& o, const Ray& ray, double* t, int* prim) {
+template <class C>
+RT_DEV bool object_t(const DevScene& sc, const DevObject& o, const Ray& ray, const RayInv& inv, double* t, int* prim) {
     if (o.geom == GEOM_SPHERE) return sphere_t(o, ray, t);
-    if (o.geom == GEOM_PLANE) return plane_t(o, ray, t);
-    return mesh_hit(sc, sc.meshes[o.mesh], ray, t, prim);
+    if (o.geom == GEOM_PLANE) return plane_t(o, ray, inv, t);
+    if constexpr (C::mesh) return mesh_hit(sc, sc.meshes[o.mesh], ray, inv, t, prim);
+    return false;
 }
 
 struct HitRec {
@@ -252,13 +349,15 @@ struct HitRec {
 };
 
 // Scene::trace_ray (scene.rs:272-289): nearest over all objects, ties to the lower index.
+template <class C>
 RT_DEV HitRec trace_closest(const DevScene& sc, const Ray& ray) {
     HitRec h{0.0, -1, -1};
+    const RayInv inv = make_inv(ray.d);
     for (int i = 0; i < sc.n_objects; ++i) {
         const DevObject& o = sc.objects[i];
         double t;
         int prim = -1;
-        if (object_t(sc, o, ray, &t, &prim)) {
+        if (object_t<C>(sc, o, ray, inv, &t, &prim)) {
             if (h.obj < 0 || t < h.t) { h.t = t; h.obj = i; h.prim = prim; }
         }
     }
@@ -266,6 +365,7 @@ RT_DEV HitRec trace_closest(const DevScene& sc, const Ray& ray) {
 }
 
 // Hit position and facing normal, computed exactly as the intersect routines build their Hit.
+template <class C>
 RT_DEV void surface(const DevScene& sc, const Ray& ray, const HitRec& h, V3* pos, V3* n) {
     const DevObject& o = sc.objects[h.obj];
     if (o.geom == GEOM_SPHERE) {
@@ -278,7 +378,7 @@ RT_DEV void surface(const DevScene& sc, const Ray& ray, const HitRec& h, V3* pos
         V3 nn = dot(pn, -ray.d) >= 0. ? pn : -pn;
         *pos = eval(ray, h.t) + nn * 0.00001;
         *n = nn;
-    } else {
+    } else if constexpr (C::mesh) {
         V3 tn = ld3(sc.tris[h.prim].n);
         V3 nn = dot(tn, -ray.d) >= 0. ? tn : -tn;
         *pos = eval(ray, h.t) + 0.00001 * nn;
@@ -289,27 +389,30 @@ RT_DEV void surface(const DevScene& sc, const Ray& ray, const HitRec& h, V3* pos
 // Scene::mutually_visible (scene.rs:258-270) as an any-hit query: occluded iff some object's
 // intersect t satisfies t + 0.001 < |y - x| (equivalent to the nearest-hit test because x + 0.001
 // rounds monotonically). Analytic objects are tested before meshes (order-free for a boolean).
+template <class C>
 RT_DEV bool visible(const DevScene& sc, V3 x, V3 y) {
     const double ERR_MARGIN = 0.001;
     V3 diff = y - x;
-    Ray r{x, norm(diff)};
     double dist = mag(diff);
-    for (int pass = 0; pass < 2; ++pass) {
+    Ray r{x, diff / dist};  // norm(diff), sharing the magnitude
+    const RayInv inv = make_inv(r.d);
+    for (int pass = 0; pass < (C::mesh ? 2 : 1); ++pass) {
         for (int i = 0; i < sc.n_objects; ++i) {
             const DevObject& o = sc.objects[i];
             if ((o.geom == GEOM_MESH) != (pass == 1)) continue;
             double t;
             int prim;
-            if (object_t(sc, o, r, &t, &prim) && !(t + ERR_MARGIN >= dist)) return false;
+            if (object_t<C>(sc, o, r, inv, &t, &prim) && !(t + ERR_MARGIN >= dist)) return false;
         }
     }
     return true;
 }
 
 // ---------------------------------------------------------------- BRDF (scene.rs:30-123)
+template <class C>
 RT_DEV V3 brdf_eval(const DevObject& o, V3 n, V3 out, V3 in) {
     if (o.brdf == BRDF_DIFFUSE) return ld3(o.k) * FRAC_1_PI;
-    if (o.brdf == BRDF_SPECULAR) {
+    if (!C::phong || o.brdf == BRDF_SPECULAR) {
         if (equal_within(in, flip_across(out, n), 0.001)) return ld3(o.k) / dot(n, in);
         return v3(0, 0, 0);
     }
@@ -325,6 +428,7 @@ RT_DEV void local_coord(V3 n, V3* u, V3* v, V3* w) {
     *v = cross(*w, *u);
 }
 // sample_incoming (scene.rs:56-98); draws: u1 = d[3], u2 = d[4], u3 = d[5].
+template <class C>
 RT_DEV void brdf_sample(const DevObject& o, V3 n, V3 out, const VertexDraws& d, V3* in, double* pdf) {
     if (o.brdf == BRDF_DIFFUSE) {
         double z = sqrt(d.v[3]);
@@ -338,7 +442,7 @@ RT_DEV void brdf_sample(const DevObject& o, V3 n, V3 out, const VertexDraws& d, 
         *pdf = dot(n, i) * FRAC_1_PI;
         return;
     }
-    if (o.brdf == BRDF_SPECULAR) {
+    if (!C::phong || o.brdf == BRDF_SPECULAR) {
         *in = flip_across(out, n);
         *pdf = 1.0;
         return;
@@ -363,9 +467,10 @@ RT_DEV void brdf_sample(const DevObject& o, V3 n, V3 out, const VertexDraws& d, 
 }
 
 // ---------------------------------------------------------------- light (geometry.rs:573-595)
+template <class C>
 RT_DEV void light_sample(const DevScene& sc, const VertexDraws& d, V3* y, V3* ny, double* pdf) {
     const DevObject& L = sc.objects[sc.light];
-    if (L.geom == GEOM_SPHERE) {
+    if (!C::mesh || L.geom == GEOM_SPHERE) {
         double xi1 = d.v[0], xi2 = d.v[1];
         double z = 2. * xi1 - 1.;
         double x = sqrt(1.0 - z * z) * cos(2. * PI * xi2);

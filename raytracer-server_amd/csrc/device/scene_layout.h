@@ -23,7 +23,9 @@ struct alignas(16) DevObject {
     double n[3];          // plane normal
     double ph_kd, ph_ks;
     double color_d[3], color_s[3];
-    int32_t emissive, pad0, pad1, pad2;  // emitted != 0 (any component)
+    int32_t emissive;     // emitted != 0 (any component)
+    int32_t axis;         // plane with n == +-e_axis exactly (0,1,2), else -1
+    int32_t pad0, pad1;
 };
 
 // Octree of one mesh, flattened in the reference's DFS pre-order (geometry.rs:1164-1216) so node
@@ -36,6 +38,7 @@ struct alignas(16) DevMesh {
     double oct_center[8][3];  // centres of the ROOT box's octants: traversal order key (geometry.rs:1249-1260)
     double surface_area;      // Mesh.surface_area (mesh-light pdf, geometry.rs:591)
     double total_weight;      // sum of triangle areas (WeightedIndex total)
+    double cull_pad;          // near_box padding: 1e-7 * max(1, |box coordinates|)
 };
 
 // Per node: x = leaf tri_ref offset (-1 for a parent), y = leaf count, z = parent node (-1 root),

@@ -9,6 +9,8 @@
 //   wavefront kernels — see wavefront_f64.hip.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "../device/integrator_f64.h"
 #include "kernels.h"
 
@@ -35,7 +37,10 @@ __device__ __forceinline__ void finalize_pixel(V3 acc, int lane, bool valid, uin
     }
 }
 
-__global__ __launch_bounds__(256) void k_megakernel_f64(DevScene sc, RenderArgs a) {
+// W = minimum waves per SIMD requested from the register allocator (0: compiler's choice).
+template <int F, int W>
+__global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderArgs a) {
+    using C = Cfg<F>;
     const int lane = threadIdx.x & 63;
     const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const long npix = (long)a.tw * a.th;
@@ -51,9 +56,9 @@ __global__ __launch_bounds__(256) void k_megakernel_f64(DevScene sc, RenderArgs 
     bool fresh = true;
     while (s < n) {
         if (fresh) begin_sample(sc, a, sp, s, ps);
-        HitRec hr = trace_closest(sc, ps.ray);
+        HitRec hr = trace_closest<C>(sc, ps.ray);
         nverts += hr.obj >= 0;
-        fresh = !shade_vertex(sc, a, sp, s, ps, hr);
+        fresh = !shade_vertex<C>(sc, a, sp, s, ps, hr);
         if (fresh) {
             acc = acc + ps.L * a.inv_n;  // server.rs:357-358
             ++s;
@@ -80,12 +85,12 @@ __global__ __launch_bounds__(256) void k_trace_f64(DevScene sc, long n, const do
     long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Ray r{v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2])};
-    HitRec h = trace_closest(sc, r);
+    HitRec h = trace_closest<Cfg<1>>(sc, r);
     obj[i] = h.obj;
     t[i] = h.obj >= 0 ? h.t : 0.0;
     if (h.obj >= 0) {
         V3 p, nn;
-        surface(sc, r, h, &p, &nn);
+        surface<Cfg<1>>(sc, r, h, &p, &nn);
         pos[3 * i] = p.x; pos[3 * i + 1] = p.y; pos[3 * i + 2] = p.z;
         nrm[3 * i] = nn.x; nrm[3 * i + 1] = nn.y; nrm[3 * i + 2] = nn.z;
     }
@@ -95,7 +100,24 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, hipStr
     long lanes = (long)a.tw * a.th * 4;
     if (lanes <= 0) return hipSuccess;
     long blocks = (lanes + 255) / 256;
-    hipLaunchKernelGGL(k_megakernel_f64, dim3((unsigned)blocks), dim3(256), 0, st, sc, a);
+    dim3 g((unsigned)blocks), b(256);
+    // 4 waves/SIMD (128 VGPRs, a few spills) measured fastest on every scene (profiles/r01_ab_waves.log);
+    // RT_MK_WAVES=2 or 1 selects the compiler's own allocation for A/B runs.
+    static const int waves = [] {
+        const char* v = std::getenv("RT_MK_WAVES");
+        return v ? std::atoi(v) : 4;
+    }();
+#define RT_MK_CASE(F)                                                                         \
+    case F:                                                                                   \
+        if (waves == 4) hipLaunchKernelGGL((k_megakernel_f64<F, 4>), g, b, 0, st, sc, a);     \
+        else if (waves == 2) hipLaunchKernelGGL((k_megakernel_f64<F, 2>), g, b, 0, st, sc, a); \
+        else hipLaunchKernelGGL((k_megakernel_f64<F, 1>), g, b, 0, st, sc, a);                \
+        break;
+    switch (a.features & 7) {
+        RT_MK_CASE(0) RT_MK_CASE(1) RT_MK_CASE(2) RT_MK_CASE(3)
+        RT_MK_CASE(4) RT_MK_CASE(5) RT_MK_CASE(6) RT_MK_CASE(7)
+    }
+#undef RT_MK_CASE
     return hipGetLastError();
 }
 

@@ -93,6 +93,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_init(DevScene sc, RenderArgs a, P
     }
 }
 
+template <int F>
 __global__ __launch_bounds__(kBlock) void k_wf_extend(DevScene sc, PathStream A, const uint32_t* cnt_in,
                                                        uint32_t* cnt_out, double* __restrict__ ht,
                                                        int32_t* __restrict__ hobj, int32_t* __restrict__ hprim) {
@@ -101,13 +102,14 @@ __global__ __launch_bounds__(kBlock) void k_wf_extend(DevScene sc, PathStream A,
     const long stride = (long)gridDim.x * blockDim.x;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         Ray r{v3(A.ox[i], A.oy[i], A.oz[i]), v3(A.dx[i], A.dy[i], A.dz[i])};
-        HitRec h = trace_closest(sc, r);
+        HitRec h = trace_closest<Cfg<F>>(sc, r);
         ht[i] = h.t;
         hobj[i] = h.obj;
         hprim[i] = h.prim;
     }
 }
 
+template <int F>
 __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, PathStream A, PathStream B,
                                                       const uint32_t* cnt_in, uint32_t* cnt_out, uint32_t* next_sub,
                                                       long nsub, const double* __restrict__ ht,
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, 
             HitRec hr{ht[i], hobj[i], hprim[i]};
             nverts += hr.obj >= 0;
             SubPixel sp = subpixel_of(a, sub);
-            emit = shade_vertex(sc, a, sp, smp, ps, hr);
+            emit = shade_vertex<Cfg<F>>(sc, a, sp, smp, ps, hr);
             if (!emit) {
                 // sample finished: sequential mean update (server.rs:357-358), then regenerate
                 double* acc = sub_buf + (size_t)sub * 3;
@@ -178,6 +180,29 @@ __global__ __launch_bounds__(kBlock) void k_wf_finalize(RenderArgs a, const doub
         a.rgb_out[p * 3 + 0] = as_u8(gc.x);
         a.rgb_out[p * 3 + 1] = as_u8(gc.y);
         a.rgb_out[p * 3 + 2] = as_u8(gc.z);
+    }
+}
+
+template <int F>
+void launch_bounce_t(dim3 g, hipStream_t st, const DevScene& sc, const RenderArgs& a, Workspace& ws, int cur, int nxt,
+                     long nsub, double* sub_buf, unsigned long long* counters) {
+    hipLaunchKernelGGL(k_wf_extend<F>, g, dim3(kBlock), 0, st, sc, ws.s[cur], ws.ctrl + cur, ws.ctrl + nxt, ws.hit_t,
+                       ws.hit_obj, ws.hit_prim);
+    hipLaunchKernelGGL(k_wf_shade<F>, g, dim3(kBlock), 0, st, sc, a, ws.s[cur], ws.s[nxt], ws.ctrl + cur,
+                       ws.ctrl + nxt, ws.ctrl + 2, nsub, ws.hit_t, ws.hit_obj, ws.hit_prim, sub_buf, counters);
+}
+
+void launch_bounce(int features, dim3 g, hipStream_t st, const DevScene& sc, const RenderArgs& a, Workspace& ws,
+                   int cur, int nxt, long nsub, double* sub_buf, unsigned long long* counters) {
+    switch (features & 7) {
+        case 0: launch_bounce_t<0>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
+        case 1: launch_bounce_t<1>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
+        case 2: launch_bounce_t<2>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
+        case 3: launch_bounce_t<3>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
+        case 4: launch_bounce_t<4>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
+        case 5: launch_bounce_t<5>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
+        case 6: launch_bounce_t<6>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
+        default: launch_bounce_t<7>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
     }
 }
 
@@ -296,11 +321,8 @@ int wavefront_render_f64(const DevScene& sc, const RenderArgs& a_in, Workspace& 
         while (true) {
             for (int k = 0; k < batch; ++k) {
                 const int nxt = cur ^ 1;
-                hipLaunchKernelGGL(k_wf_extend, dim3((unsigned)grid), dim3(kBlock), 0, st, sc, ws.s[cur],
-                                   ws.ctrl + cur, ws.ctrl + nxt, ws.hit_t, ws.hit_obj, ws.hit_prim);
-                hipLaunchKernelGGL(k_wf_shade, dim3((unsigned)grid), dim3(kBlock), 0, st, sc, a, ws.s[cur], ws.s[nxt],
-                                   ws.ctrl + cur, ws.ctrl + nxt, ws.ctrl + 2, nsub, ws.hit_t, ws.hit_obj,
-                                   ws.hit_prim, sub_buf, stats ? ws.counters : nullptr);
+                launch_bounce(a.features, dim3((unsigned)grid), st, sc, a, ws, cur, nxt, nsub, sub_buf,
+                              stats ? ws.counters : nullptr);
                 cur = nxt;
                 ++iters;
             }

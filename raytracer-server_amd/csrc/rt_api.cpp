@@ -100,6 +100,11 @@ void pack_scene(rt_scene* s) {
             dm.oct_center[i][2] = (lo.z + hi.z) / 2.0;
         }
         dm.surface_area = m.surface_area;
+        {
+            double mx = 1.0;
+            for (double v : rbox) mx = std::fmax(mx, std::fabs(v));
+            dm.cull_pad = 1e-7 * mx;
+        }
         double cum = 0.0;
         for (size_t t = 0; t < m.num_triangles(); ++t) {
             D3 a = m.vertices[m.indices[3 * t]], b = m.vertices[m.indices[3 * t + 1]], cc = m.vertices[m.indices[3 * t + 2]];
@@ -153,6 +158,14 @@ void pack_scene(rt_scene* s) {
         cp3(d.color_d, o.color_d);
         cp3(d.color_s, o.color_s);
         d.emissive = (o.emitted.x != 0.0 || o.emitted.y != 0.0 || o.emitted.z != 0.0) ? 1 : 0;
+        d.axis = -1;
+        if (o.geom == RT_GEOM_PLANE) {
+            const double n3[3] = {o.n.x, o.n.y, o.n.z};
+            int nz = 0, ax = -1;
+            for (int k = 0; k < 3; ++k)
+                if (n3[k] != 0.0) { ++nz; ax = k; }
+            if (nz == 1 && std::fabs(n3[ax]) == 1.0) d.axis = ax;
+        }
         p.objects.push_back(d);
     }
 }
@@ -256,6 +269,11 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
     a.th = p->tile_h;
     a.n_samples = p->spp > 0 ? p->spp / 4 : 0;  // server.rs:332 (i32 division)
     a.mis = (p->flags & RT_FLAG_MIS) ? 1 : 0;
+    {
+        bool phong = false;
+        for (const auto& o : s->host.objects) phong |= o.brdf == RT_BRDF_PHONG;
+        a.features = (s->host.meshes.empty() ? 0 : 1) | (phong ? 2 : 0) | (a.mis ? 4 : 0);
+    }
     a.seed = p->seed;
     rt::host::camera_frame(s->host, p->width, p->height, a.cx, a.cy);
     a.inv_n = a.n_samples > 0 ? 1. / (double)a.n_samples : 0.0;

@@ -1,0 +1,7 @@
+#!/bin/bash
+# PMC passes on the megakernel (cornell, 1920x1080, 64 spp)
+export TMPDIR=/tmp
+P="python tools/prof_render.py cornell_box 1920 1080 64 mk"
+timeout -k 10 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU -d gpurun_out/pmc1 -o run --output-format csv -- $P > gpurun_out/pmc1.log 2>&1; echo p1=$?
+timeout -k 10 200 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 -d gpurun_out/pmc2 -o run --output-format csv -- $P > gpurun_out/pmc2.log 2>&1; echo p2=$?
+timeout -k 10 200 rocprofv3 --pmc SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INST_CYCLES_SALU SQ_INST_CYCLES_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_INST_LEVEL_SMEM -d gpurun_out/pmc3 -o run --output-format csv -- $P > gpurun_out/pmc3.log 2>&1; echo p3=$?

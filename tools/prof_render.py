@@ -1,0 +1,20 @@
+"""One render through the C ABI for profiling runs: python tools/prof_render.py SCENE W H SPP [mk|wf] [mis]"""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "raytracer-server_amd"))
+import rt_amd  # noqa: E402
+
+scene, w, h, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+mode = sys.argv[5] if len(sys.argv) > 5 else "mk"
+mis = len(sys.argv) > 6 and sys.argv[6] == "mis"
+s = rt_amd.Scene.from_toml(os.path.join(REPO, "scenes", f"{scene}.toml"))
+t = time.perf_counter()
+rgb, _, st = rt_amd.render(s, w, h, spp, megakernel=(mode == "mk"), mis=mis)
+dt = time.perf_counter() - t
+n = w * h * 4 * (spp // 4)
+print(f"{scene} {w}x{h}x{spp} {mode}{' mis' if mis else ''}: {dt*1e3:.1f} ms wall, {st['device_ms']:.1f} ms device, "
+      f"{n / st['device_ms'] / 1e3:.1f} Msamples/s, {st['vertices'] / max(1, n):.3f} vertices/sample, "
+      f"iterations {st['iterations']}")
