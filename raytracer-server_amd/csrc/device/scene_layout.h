@@ -53,6 +53,13 @@ struct DevTri {
     double a[3], ab[3], ac[3], n[3];
 };
 
+// Compact per-type object tables, passed in the kernel arguments so the trace loops are unrolled
+// and their operands live in scalar registers (no per-object loads or type branches). Objects keep
+// their scene index for the reference's tie rule (scene.rs:278: ties go to the lower index).
+constexpr int kMaxAxisPlanes = 6;  // per axis
+constexpr int kMaxSpheres = 6;
+constexpr int kMaxGeneric = 8;     // meshes and non-axis planes
+
 struct DevScene {
     const DevObject* objects;
     const DevMesh* meshes;
@@ -64,6 +71,15 @@ struct DevScene {
     const double* tri_cum_area;  // per triangle, cumulative area within its mesh (mesh-light pick)
     int32_t n_objects, light, n_meshes, mesh_order_last;  // mesh_order_last: test meshes after analytic objects
     double cam_pos[3], cam_dir[3];
+    // compact tables (valid when `compact`; see Cfg::compact)
+    int32_t compact;
+    int32_t n_ax[3];                         // planes with n = +-e_k, per axis k
+    int32_t n_sph, n_gen;
+    int32_t ax_idx[3][kMaxAxisPlanes];
+    double ax_pos[3][kMaxAxisPlanes];        // plane point coordinate along its axis
+    int32_t sph_idx[kMaxSpheres];
+    double sph[kMaxSpheres][4];              // centre xyz, r*r
+    int32_t gen_idx[kMaxGeneric];            // everything else, through the generic intersector
 };
 
 }  // namespace rt

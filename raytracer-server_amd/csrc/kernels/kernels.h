@@ -22,7 +22,9 @@ struct RenderArgs {
     unsigned long long* counters;  // optional [0] = path vertices
 };
 
-hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, hipStream_t st);
+hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
+                                 hipStream_t st);
+hipError_t launch_finalize_f64(const RenderArgs& a, const double* sub_buf, hipStream_t st);
 hipError_t launch_trace_f64(const DevScene& sc, long n, const double* o, const double* d, double* t, int32_t* obj,
                             double* pos, double* nrm, hipStream_t st);
 

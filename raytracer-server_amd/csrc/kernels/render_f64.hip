@@ -1,14 +1,11 @@
 // f64 render kernels for gfx950 (CDNA4).
 //
-//   k_megakernel_f64  — fused path loop: one lane owns one subpixel (server.rs:335-336) and walks
-//                       its spp/4 sample paths vertex by vertex; a lane whose path ends starts its
-//                       next sample in the same iteration (regeneration), so a wave idles only in
-//                       the final tail. Accumulation per subpixel is sequential in sample order,
-//                       exactly the reference's order (server.rs:338-358).
+//   k_megakernel_f64  — fused, persistent path loop (below); k_finalize_f64 — subpixel means -> RGB8.
 //   k_trace_f64       — Scene::trace_ray for a batch of rays (parity tests of the intersectors).
 //   wavefront kernels — see wavefront_f64.hip.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "../device/integrator_f64.h"
@@ -17,65 +14,90 @@
 namespace rt {
 using namespace f64;
 
-// Per-pixel finalisation from the 4 subpixel means held by 4 consecutive lanes
-// (server.rs:360 clamp-then-average, :366-368 gamma, :187-189 `as u8`).
-__device__ __forceinline__ void finalize_pixel(V3 acc, int lane, bool valid, uint8_t* rgb, size_t pix) {
-    int base = lane & ~3;
-    V3 pixel = v3(0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        V3 a = v3(__shfl(acc.x, base + j, 64), __shfl(acc.y, base + j, 64), __shfl(acc.z, base + j, 64));
-        pixel = pixel + clampv(a, 0., 1.) * 0.25;
-    }
-    if (valid && (lane & 3) == 0) {
-        V3 c = clampv(pixel, 0., 1.);
-        const double g = 1.0 / 2.2;
-        V3 gc = v3(pow(c.x, g), pow(c.y, g), pow(c.z, g)) * 255.0 + v3(0.5, 0.5, 0.5);
-        rgb[pix * 3 + 0] = as_u8(gc.x);
-        rgb[pix * 3 + 1] = as_u8(gc.y);
-        rgb[pix * 3 + 2] = as_u8(gc.z);
-    }
+// Wave-aggregated ticket: every lane with `want` gets the next value of *counter (one atomic per
+// wave). All 64 lanes must call it together.
+__device__ __forceinline__ long wave_ticket(uint32_t* counter, bool want) {
+    const unsigned long long m = __ballot(want);
+    if (m == 0ull) return -1;
+    const int lane = __lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+    return want ? (long)base + __popcll(below) : -1;
 }
 
-// W = minimum waves per SIMD requested from the register allocator (0: compiler's choice).
+// Persistent megakernel: a resident grid whose lanes pull subpixels from a global counter. A lane
+// walks the spp/4 sample paths of its subpixel vertex by vertex; when a path ends, the next sample
+// starts in the same iteration (regeneration); when the subpixel is done its mean goes to
+// sub_buf (sequential sum in sample order, server.rs:338-358) and the lane takes the next
+// subpixel. Waves idle only in the frame's final tail, not per wave.
+// W = minimum waves per SIMD requested from the register allocator.
 template <int F, int W>
-__global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderArgs a) {
+__global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
+                                                          uint32_t* next_sub, long nsub) {
     using C = Cfg<F>;
     const int lane = threadIdx.x & 63;
-    const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long npix = (long)a.tw * a.th;
-    const long pix = q >> 2;
-    const bool valid = pix < npix;
-    const SubPixel sp = subpixel_of(a, valid ? q : 0);
-
-    V3 acc = v3(0, 0, 0);
     unsigned long long nverts = 0;
-    const int n = valid ? a.n_samples : 0;
+    long id = wave_ticket(next_sub, true);
+    bool active = id < nsub;
+    SubPixel sp = subpixel_of(a, active ? id : 0);
+    V3 acc = v3(0, 0, 0);
     int s = 0;
     PathState ps;
     bool fresh = true;
-    while (s < n) {
-        if (fresh) begin_sample(sc, a, sp, s, ps);
-        HitRec hr = trace_closest<C>(sc, ps.ray);
-        nverts += hr.obj >= 0;
-        fresh = !shade_vertex<C>(sc, a, sp, s, ps, hr);
-        if (fresh) {
-            acc = acc + ps.L * a.inv_n;  // server.rs:357-358
-            ++s;
+    while (__any(active)) {
+        bool done = false;
+        if (active) {
+            if (fresh) begin_sample(sc, a, sp, s, ps);
+            HitRec hr = trace_closest<C>(sc, ps.ray);
+            nverts += hr.obj >= 0;
+            fresh = !shade_vertex<C>(sc, a, sp, s, ps, hr);
+            if (fresh) {
+                acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                if (++s == a.n_samples) {
+                    double* o = sub_buf + (size_t)id * 3;
+                    o[0] = acc.x;
+                    o[1] = acc.y;
+                    o[2] = acc.z;
+                    done = true;
+                }
+            }
+        }
+        long nid = wave_ticket(next_sub, done);
+        if (done) {
+            id = nid;
+            active = id < nsub;
+            if (active) sp = subpixel_of(a, id);
+            acc = v3(0, 0, 0);
+            s = 0;
+            fresh = true;
         }
     }
-    if (valid && a.sub_out) {
-        double* so = a.sub_out + ((size_t)pix * 4 + sp.sub) * 3;
-        so[0] = acc.x;
-        so[1] = acc.y;
-        so[2] = acc.z;
-    }
-    finalize_pixel(acc, lane, valid, a.rgb_out, (size_t)pix);
     if (a.counters) {
         unsigned long long v = nverts;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        if (lane == 0) atomicAdd(a.counters, v);
+        if (lane == 0 && v) atomicAdd(a.counters, v);
+    }
+}
+
+// 4 subpixel means -> RGB8 (server.rs:360 clamp-then-average, :366-368 gamma, :187-189 `as u8`).
+__global__ __launch_bounds__(256) void k_finalize_f64(RenderArgs a, const double* __restrict__ sub_buf) {
+    const long npix = (long)a.tw * a.th;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += stride) {
+        const double* s = sub_buf + (size_t)p * 12;
+        V3 pixel = v3(0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pixel = pixel + clampv(v3(s[3 * j], s[3 * j + 1], s[3 * j + 2]), 0., 1.) * 0.25;
+        V3 c = clampv(pixel, 0., 1.);
+        const double g = 1.0 / 2.2;
+        V3 gc = v3(pow(c.x, g), pow(c.y, g), pow(c.z, g)) * 255.0 + v3(0.5, 0.5, 0.5);
+        a.rgb_out[p * 3 + 0] = as_u8(gc.x);
+        a.rgb_out[p * 3 + 1] = as_u8(gc.y);
+        a.rgb_out[p * 3 + 2] = as_u8(gc.z);
     }
 }
 
@@ -96,28 +118,43 @@ __global__ __launch_bounds__(256) void k_trace_f64(DevScene sc, long n, const do
     }
 }
 
-hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, hipStream_t st) {
-    long lanes = (long)a.tw * a.th * 4;
-    if (lanes <= 0) return hipSuccess;
-    long blocks = (lanes + 255) / 256;
-    dim3 g((unsigned)blocks), b(256);
-    // 4 waves/SIMD (128 VGPRs, a few spills) measured fastest on every scene (profiles/r01_ab_waves.log);
-    // RT_MK_WAVES=2 or 1 selects the compiler's own allocation for A/B runs.
+hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
+                                 hipStream_t st) {
+    const long nsub = (long)a.tw * a.th * 4;
+    if (nsub <= 0 || a.n_samples <= 0) return hipSuccess;
+    // 4 waves/SIMD (128 VGPRs) measured fastest on every scene (profiles/r01_ab_waves.log);
+    // RT_MK_WAVES=1 selects the compiler's own allocation for A/B runs.
     static const int waves = [] {
         const char* v = std::getenv("RT_MK_WAVES");
         return v ? std::atoi(v) : 4;
     }();
-#define RT_MK_CASE(F)                                                                         \
-    case F:                                                                                   \
-        if (waves == 4) hipLaunchKernelGGL((k_megakernel_f64<F, 4>), g, b, 0, st, sc, a);     \
-        else if (waves == 2) hipLaunchKernelGGL((k_megakernel_f64<F, 2>), g, b, 0, st, sc, a); \
-        else hipLaunchKernelGGL((k_megakernel_f64<F, 1>), g, b, 0, st, sc, a);                \
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const long resident = (long)ncu * (waves == 4 ? 4 : 2);  // 256-thread blocks per CU at that occupancy
+    const long blocks = std::max(1L, std::min(resident, (nsub + 255) / 256));
+    hipError_t e = hipMemsetAsync(next_sub, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    dim3 g((unsigned)blocks), b(256);
+#define RT_MK_CASE(F)                                                                                  \
+    case F:                                                                                            \
+        if (waves == 4) hipLaunchKernelGGL((k_megakernel_f64<F, 4>), g, b, 0, st, sc, a, sub_buf, next_sub, nsub); \
+        else hipLaunchKernelGGL((k_megakernel_f64<F, 1>), g, b, 0, st, sc, a, sub_buf, next_sub, nsub);            \
         break;
-    switch (a.features & 7) {
-        RT_MK_CASE(0) RT_MK_CASE(1) RT_MK_CASE(2) RT_MK_CASE(3)
-        RT_MK_CASE(4) RT_MK_CASE(5) RT_MK_CASE(6) RT_MK_CASE(7)
+    switch (a.features & 15) {
+        RT_MK_CASE(0) RT_MK_CASE(1) RT_MK_CASE(2) RT_MK_CASE(3) RT_MK_CASE(4) RT_MK_CASE(5) RT_MK_CASE(6)
+        RT_MK_CASE(7) RT_MK_CASE(8) RT_MK_CASE(9) RT_MK_CASE(10) RT_MK_CASE(11) RT_MK_CASE(12) RT_MK_CASE(13)
+        RT_MK_CASE(14) RT_MK_CASE(15)
     }
 #undef RT_MK_CASE
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize_f64(const RenderArgs& a, const double* sub_buf, hipStream_t st) {
+    const long npix = (long)a.tw * a.th;
+    if (npix <= 0) return hipSuccess;
+    const long blocks = std::max(1L, std::min(2048L, (npix + 255) / 256));
+    hipLaunchKernelGGL(k_finalize_f64, dim3((unsigned)blocks), dim3(256), 0, st, a, sub_buf);
     return hipGetLastError();
 }
 

@@ -166,23 +166,6 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, 
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_wf_finalize(RenderArgs a, const double* __restrict__ sub_buf) {
-    const long npix = (long)a.tw * a.th;
-    const long stride = (long)gridDim.x * blockDim.x;
-    for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += stride) {
-        const double* s = sub_buf + (size_t)p * 12;
-        V3 pixel = v3(0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) pixel = pixel + clampv(v3(s[3 * j], s[3 * j + 1], s[3 * j + 2]), 0., 1.) * 0.25;
-        V3 c = clampv(pixel, 0., 1.);
-        const double g = 1.0 / 2.2;
-        V3 gc = v3(pow(c.x, g), pow(c.y, g), pow(c.z, g)) * 255.0 + v3(0.5, 0.5, 0.5);
-        a.rgb_out[p * 3 + 0] = as_u8(gc.x);
-        a.rgb_out[p * 3 + 1] = as_u8(gc.y);
-        a.rgb_out[p * 3 + 2] = as_u8(gc.z);
-    }
-}
-
 template <int F>
 void launch_bounce_t(dim3 g, hipStream_t st, const DevScene& sc, const RenderArgs& a, Workspace& ws, int cur, int nxt,
                      long nsub, double* sub_buf, unsigned long long* counters) {
@@ -194,16 +177,14 @@ void launch_bounce_t(dim3 g, hipStream_t st, const DevScene& sc, const RenderArg
 
 void launch_bounce(int features, dim3 g, hipStream_t st, const DevScene& sc, const RenderArgs& a, Workspace& ws,
                    int cur, int nxt, long nsub, double* sub_buf, unsigned long long* counters) {
-    switch (features & 7) {
-        case 0: launch_bounce_t<0>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
-        case 1: launch_bounce_t<1>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
-        case 2: launch_bounce_t<2>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
-        case 3: launch_bounce_t<3>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
-        case 4: launch_bounce_t<4>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
-        case 5: launch_bounce_t<5>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
-        case 6: launch_bounce_t<6>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
-        default: launch_bounce_t<7>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
+#define RT_WF_CASE(F) \
+    case F: launch_bounce_t<F>(g, st, sc, a, ws, cur, nxt, nsub, sub_buf, counters); break;
+    switch (features & 15) {
+        RT_WF_CASE(0) RT_WF_CASE(1) RT_WF_CASE(2) RT_WF_CASE(3) RT_WF_CASE(4) RT_WF_CASE(5) RT_WF_CASE(6)
+        RT_WF_CASE(7) RT_WF_CASE(8) RT_WF_CASE(9) RT_WF_CASE(10) RT_WF_CASE(11) RT_WF_CASE(12) RT_WF_CASE(13)
+        RT_WF_CASE(14) RT_WF_CASE(15)
     }
+#undef RT_WF_CASE
 }
 
 size_t env_size(const char* name, size_t dflt) {
@@ -352,9 +333,7 @@ int wavefront_render_f64(const DevScene& sc, const RenderArgs& a_in, Workspace& 
         if ((e = hipMemsetAsync(sub_buf, 0, (size_t)npix * 12 * sizeof(double), st)) != hipSuccess)
             return hip_fail(e, "memset");
     }
-    const long fgrid = std::max<long>(1, std::min<long>(grid_cap, (npix + kBlock - 1) / kBlock));
-    hipLaunchKernelGGL(k_wf_finalize, dim3((unsigned)fgrid), dim3(kBlock), 0, st, a, (const double*)sub_buf);
-    if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "k_wf_finalize");
+    if ((e = launch_finalize_f64(a, sub_buf, st)) != hipSuccess) return hip_fail(e, "finalize");
     if (stats) {
         unsigned long long c[1] = {0};
         if ((e = hipMemcpyAsync(c, ws.counters, sizeof c, hipMemcpyDeviceToHost, st)) != hipSuccess)

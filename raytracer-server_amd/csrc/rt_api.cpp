@@ -170,6 +170,36 @@ void pack_scene(rt_scene* s) {
     }
 }
 
+// Groups objects for the compact trace (axis planes per axis, spheres, everything else).
+void fill_compact(const Packed& p, rt::DevScene* ds) {
+    int nax[3] = {0, 0, 0}, ns = 0, ng = 0;
+    bool ok = true;
+    for (size_t i = 0; i < p.objects.size(); ++i) {
+        const rt::DevObject& o = p.objects[i];
+        if (o.geom == rt::GEOM_PLANE && o.axis >= 0) {
+            if (nax[o.axis] == rt::kMaxAxisPlanes) { ok = false; break; }
+            ds->ax_idx[o.axis][nax[o.axis]] = (int32_t)i;
+            ds->ax_pos[o.axis][nax[o.axis]] = o.pos[o.axis];
+            ++nax[o.axis];
+        } else if (o.geom == rt::GEOM_SPHERE) {
+            if (ns == rt::kMaxSpheres) { ok = false; break; }
+            ds->sph_idx[ns] = (int32_t)i;
+            ds->sph[ns][0] = o.pos[0];
+            ds->sph[ns][1] = o.pos[1];
+            ds->sph[ns][2] = o.pos[2];
+            ds->sph[ns][3] = o.r * o.r;
+            ++ns;
+        } else {
+            if (ng == rt::kMaxGeneric) { ok = false; break; }
+            ds->gen_idx[ng++] = (int32_t)i;
+        }
+    }
+    ds->compact = ok ? 1 : 0;
+    for (int k = 0; k < 3; ++k) ds->n_ax[k] = ok ? nax[k] : 0;
+    ds->n_sph = ok ? ns : 0;
+    ds->n_gen = ok ? ng : 0;
+}
+
 template <class T>
 void put(std::vector<char>& blob, size_t* off, const std::vector<T>& v) {
     *off = align_up(blob.size(), 256);
@@ -211,6 +241,7 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.tris = (const rt::DevTri*)(b + o_tris);
         ds.tri_cum_area = (const double*)(b + o_cum);
         ds.n_objects = (int32_t)p.objects.size();
+        fill_compact(p, &ds);
         ds.light = s->host.light;
         ds.n_meshes = (int32_t)p.meshes.size();
         cp3(ds.cam_pos, s->host.cam_pos);
@@ -272,7 +303,7 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
     {
         bool phong = false;
         for (const auto& o : s->host.objects) phong |= o.brdf == RT_BRDF_PHONG;
-        a.features = (s->host.meshes.empty() ? 0 : 1) | (phong ? 2 : 0) | (a.mis ? 4 : 0);
+        a.features = (s->host.meshes.empty() ? 0 : 1) | (phong ? 2 : 0) | (a.mis ? 4 : 0) | (ds.compact ? 8 : 0);
     }
     a.seed = p->seed;
     rt::host::camera_frame(s->host, p->width, p->height, a.cx, a.cy);
@@ -291,12 +322,20 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
     int out = RT_OK;
     std::string err;
     if (p->flags & RT_FLAG_MEGAKERNEL) {
+        const size_t npix = (size_t)p->tile_w * p->tile_h;
         hipError_t e = ws->ensure_counters();
+        double* sub = d_sub;
+        if (e == hipSuccess && !sub) {
+            e = ws->ensure_sub(npix);
+            sub = ws->sub_buf;
+        }
         if (e == hipSuccess && stats) e = hipMemsetAsync(ws->counters, 0, 8 * sizeof(unsigned long long), st);
+        if (e == hipSuccess && a.n_samples <= 0) e = hipMemsetAsync(sub, 0, npix * 12 * sizeof(double), st);
         if (e == hipSuccess) {
             a.counters = stats ? ws->counters : nullptr;
-            e = rt::launch_megakernel_f64(ds, a, st);
+            e = rt::launch_megakernel_f64(ds, a, sub, (uint32_t*)(ws->counters + 4), st);
         }
+        if (e == hipSuccess) e = rt::launch_finalize_f64(a, sub, st);
         if (e != hipSuccess) { out = RT_E_HIP; err = std::string("megakernel: ") + hipGetErrorString(e); }
     } else {
         out = rt::wavefront_render_f64(ds, a, *ws, st, cancel, stats, &err);
