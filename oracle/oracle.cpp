@@ -99,10 +99,14 @@ struct Hit {
     int id;
 };
 
-// ---- RNG spec (shared with the HIP kernels) ----
-// Philox4x32-10 (Salmon et al., SC'11; Random123 constants) keyed by the 64-bit seed, counter
-// (pixel, sample, depth, subpixel); its 128-bit output seeds xoroshiro128++ whose k-th output is
-// draw slot k. uniform = (u64 >> 11) * 2^-53 (rand 0.8's f64 conversion).
+// ---- RNG spec v2 (shared with the HIP kernels) ----
+// One stream per camera sample: Philox4x32-10 (Salmon et al., SC'11; Random123 constants) keyed
+// by the 64-bit seed with counter (pixel, sample, 0, subpixel) seeds xoroshiro128++, whose outputs
+// are consumed in the reference's own draw order along the path (thread_rng is likewise consumed
+// sequentially): camera r1, r2 (server.rs:339,346); per diffuse vertex light xi1, xi2
+// (geometry.rs:576-577; a mesh light draws its triangle pick first, :589), RR (scene.rs:231),
+// BSDF u1, u2 (scene.rs:59,61; Phong u, xi1, xi2); per mirror vertex RR (scene.rs:173).
+// uniform = (u64 >> 11) * 2^-53 (rand 0.8's f64 conversion).
 static inline void philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
     uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
     uint32_t k0 = key_in[0], k1 = key_in[1];
@@ -121,26 +125,17 @@ static inline void philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-enum {
-    SLOT_CAM_R1 = 0, SLOT_CAM_R2 = 1,              // depth 0
-    SLOT_LIGHT_XI1 = 0, SLOT_LIGHT_XI2 = 1,        // every vertex
-    SLOT_RR = 2, SLOT_BSDF_U1 = 3, SLOT_BSDF_U2 = 4, SLOT_BSDF_U3 = 5,
-    SLOT_LIGHT_PICK = 6
-};
-
 struct Rng {
     uint64_t s0, s1;
-    double cache[8];
-    int n;
-    Rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t depth, uint32_t sub) {
-        uint32_t ctr[4] = {pixel, sample, depth, sub};
+    Rng() : s0(1), s1(0) {}
+    Rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t sub) {
+        uint32_t ctr[4] = {pixel, sample, 0u, sub};
         uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
         uint32_t o[4];
         philox4x32_10(ctr, key, o);
         s0 = ((uint64_t)o[0] << 32) | o[1];
         s1 = ((uint64_t)o[2] << 32) | o[3];
         if ((s0 | s1) == 0) s0 = 1;
-        n = 0;
     }
     static inline uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
     uint64_t next() {  // xoroshiro128++ (Blackman & Vigna 2019)
@@ -151,10 +146,7 @@ struct Rng {
         s1 = rotl(b, 28);
         return r;
     }
-    double slot(int k) {
-        while (n <= k) cache[n++] = (double)(next() >> 11) * (1.0 / 9007199254740992.0);
-        return cache[k];
-    }
+    double uniform() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
 };
 
 // ---- geometry.rs:916-1113 BoundingBox ----
@@ -407,9 +399,9 @@ static void create_local_coord(V3 n, V3* u, V3* v, V3* w) {  // scene.rs:112
 static void brdf_sample(const Object& o, V3 n, V3 out, Rng& rng, V3* in, double* pdf) {  // scene.rs:56
     switch (o.brdf) {
         case BRDF_DIFFUSE: {
-            double z = std::sqrt(rng.slot(SLOT_BSDF_U1));
+            double z = std::sqrt(rng.uniform());
             double r = std::sqrt(1.0 - z * z);
-            double phi = 2.0 * PI * rng.slot(SLOT_BSDF_U2);
+            double phi = 2.0 * PI * rng.uniform();
             double x = r * std::cos(phi), y = r * std::sin(phi);
             V3 u, v, w;
             create_local_coord(n, &u, &v, &w);
@@ -424,14 +416,14 @@ static void brdf_sample(const Object& o, V3 n, V3 out, Rng& rng, V3* in, double*
             return;
         default: {
             double p = (double)o.ph_power;
-            double u = rng.slot(SLOT_BSDF_U1);
+            double u = rng.uniform();
             if (u < o.ph_kd) {
-                double xi1 = rng.slot(SLOT_BSDF_U2), xi2 = rng.slot(SLOT_BSDF_U3);
+                double xi1 = rng.uniform(), xi2 = rng.uniform();
                 V3 i = v3(std::sqrt(1. - xi1) * std::cos(2. * PI * xi2), std::sqrt(1. - xi1) * std::sin(2. * PI * xi2), std::sqrt(xi1));
                 *in = i;
                 *pdf = dot(n, i) * FRAC_1_PI;
             } else if (o.ph_kd <= u && u < o.ph_kd + o.ph_ks) {
-                double xi1 = rng.slot(SLOT_BSDF_U2), xi2 = rng.slot(SLOT_BSDF_U3);
+                double xi1 = rng.uniform(), xi2 = rng.uniform();
                 V3 i = v3(std::sqrt(1. - std::pow(xi1, 2. / (p + 1.))) * std::cos(2. * PI * xi2),
                           std::sqrt(1. - std::pow(xi1, 2. / (p + 1.))) * std::sin(2. * PI * xi2),
                           std::pow(xi1, 1. / (p + 1.)));
@@ -502,7 +494,7 @@ static bool trace_ray(const Scene& s, const Ray& ray, Hit* nh) {  // scene.rs:27
 static void light_sample(const Scene& s, Rng& rng, V3* y, V3* ny, double* pdf) {
     const Object& L = s.objects[s.light];
     if (L.geom == GEOM_SPHERE) {
-        double xi1 = rng.slot(SLOT_LIGHT_XI1), xi2 = rng.slot(SLOT_LIGHT_XI2);
+        double xi1 = rng.uniform(), xi2 = rng.uniform();
         double z = 2. * xi1 - 1.;
         double x = std::sqrt(1.0 - z * z) * std::cos(2. * PI * xi2);
         double yy = std::sqrt(1.0 - z * z) * std::sin(2. * PI * xi2);
@@ -516,7 +508,7 @@ static void light_sample(const Scene& s, Rng& rng, V3* y, V3* ny, double* pdf) {
         const Mesh& m = s.meshes[L.mesh];
         double total = 0;
         for (double a : m.areas) total += a;
-        double u = rng.slot(SLOT_LIGHT_PICK) * total;
+        double u = rng.uniform() * total;
         double acc = 0;
         size_t idx = m.areas.size() - 1;
         for (size_t i = 0; i < m.areas.size(); ++i) {
@@ -524,8 +516,8 @@ static void light_sample(const Scene& s, Rng& rng, V3* y, V3* ny, double* pdf) {
             if (acc > u) { idx = i; break; }
         }
         Tri t = m.tri(idx);
-        double b0 = 1. - std::sqrt(rng.slot(SLOT_LIGHT_XI1));
-        double b1 = (1. - b0) * rng.slot(SLOT_LIGHT_XI2);
+        double b0 = 1. - std::sqrt(rng.uniform());
+        double b1 = (1. - b0) * rng.uniform();
         V3 ab = norm(t.b - t.a), ac = norm(t.c - t.a);
         *y = ab * b0 + ac * b1;
         *ny = tri_normal(t);
@@ -555,8 +547,7 @@ static bool mutually_visible(const Scene& s, V3 x, V3 y) {  // scene.rs:258
 
 struct Ctx {
     const Scene* s;
-    uint64_t seed;
-    uint32_t pixel, sample, sub;
+    Rng rng;  // this sample's stream
     bool mis;
     uint64_t vertices, casts;
 };
@@ -573,10 +564,10 @@ static V3 reflected(Ctx& c, const Hit& hit, V3 o, uint64_t depth) {
     V3 x = hit.pos, n = hit.n;
     const Object& obj = s.objects[hit.id];
     double p = depth <= MAX_BOUNCES ? 1.0 : SURVIVAL_PROBABILITY;
-    Rng rng(c.seed, c.pixel, c.sample, (uint32_t)depth, c.sub);
+    Rng& rng = c.rng;
     if (obj.brdf == BRDF_SPECULAR) {
         V3 rad = v3(0, 0, 0);
-        if (rng.slot(SLOT_RR) < p) {
+        if (rng.uniform() < p) {
             V3 i; double pdf;
             brdf_sample(obj, n, o, rng, &i, &pdf);
             Hit h2;
@@ -612,7 +603,7 @@ static V3 reflected(Ctx& c, const Hit& hit, V3 o, uint64_t depth) {
             }
         }
     }
-    if (rng.slot(SLOT_RR) < p) {
+    if (rng.uniform() < p) {
         V3 i; double pdf_brdf;
         brdf_sample(obj, n, o, rng, &i, &pdf_brdf);
         Hit h2;
@@ -651,17 +642,16 @@ static V3 sample_pixel(const Scene& s, int x, int y, int width, int height, int 
     V3 cy = norm(cross(cx, s.camera.dir)) * 0.5135;
     int num_samples = spp / 4;
     V3 pixel = v3(0, 0, 0);
-    Ctx c{&s, seed, pixel_id, 0, 0, mis, 0, 0};
+    Ctx c{&s, Rng(), mis, 0, 0};
     for (int sy = 0; sy < 2; ++sy) {
         for (int sx = 0; sx < 2; ++sx) {
             V3 rad = v3(0, 0, 0);
-            c.sub = (uint32_t)(sy * 2 + sx);
+            const uint32_t sub = (uint32_t)(sy * 2 + sx);
             for (int smp = 0; smp < num_samples; ++smp) {
-                c.sample = (uint32_t)smp;
-                Rng rng(seed, pixel_id, (uint32_t)smp, 0, c.sub);
-                double r1 = 2. * rng.slot(SLOT_CAM_R1);
+                c.rng = Rng(seed, pixel_id, (uint32_t)smp, sub);
+                double r1 = 2. * c.rng.uniform();
                 double dx = r1 < 1. ? std::sqrt(r1) - 1. : 1. - std::sqrt(2. - r1);
-                double r2 = 2. * rng.slot(SLOT_CAM_R2);
+                double r2 = 2. * c.rng.uniform();
                 double dy = r2 < 1. ? std::sqrt(r2) - 1. : 1. - std::sqrt(2. - r2);
                 V3 d = cx * ((((double)sx + 0.5 + dx) / 2. + (double)x) / w - 0.5) +
                        cy * ((((double)sy + 0.5 + dy) / 2. + (double)y) / h - 0.5) + s.camera.dir;
@@ -947,9 +937,9 @@ void orc_octants(const double mn[3], const double mx[3], double out[48]) {
 }
 
 void orc_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) { philox4x32_10(ctr, key, out); }
-void orc_draws(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t depth, uint32_t sub, int n, double* out) {
-    Rng r(seed, pixel, sample, depth, sub);
-    for (int k = 0; k < n && k < 8; ++k) out[k] = r.slot(k);
+void orc_draws(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t sub, int n, double* out) {
+    Rng r(seed, pixel, sample, sub);
+    for (int k = 0; k < n; ++k) out[k] = r.uniform();
 }
 
 // Scene::trace_ray for a batch of rays: t, object id (-1 miss), hit pos[3], n[3].

@@ -26,6 +26,7 @@ struct PathState {
     Ray ray;
     V3 beta, L, bemit, o;
     double pdf_prev;
+    uint64_t r0, r1;  // this sample's RNG stream (xoroshiro128++ state)
     uint32_t depth;
     int kind;
 };
@@ -50,8 +51,10 @@ RT_DEV SubPixel subpixel_of(const RenderArgs& a, long p) {
 
 // New camera path for sample `smp` of subpixel `sp` (server.rs:338-357).
 RT_DEV void begin_sample(const DevScene& sc, const RenderArgs& a, const SubPixel& sp, int smp, PathState& ps) {
-    Rng rng(a.seed, sp.pid, (uint32_t)smp, 0u, (uint32_t)sp.sub);
+    Rng rng(a.seed, sp.pid, (uint32_t)smp, (uint32_t)sp.sub);
     double u1 = rng.uniform(), u2 = rng.uniform();
+    ps.r0 = rng.s0;
+    ps.r1 = rng.s1;
     ps.ray = camera_ray(sc, ld3(a.cx), ld3(a.cy), (double)a.width, (double)a.height, sp.col, sp.yref, sp.sx, sp.sy, u1, u2);
     ps.beta = v3(1, 1, 1);
     ps.L = v3(0, 0, 0);
@@ -86,14 +89,15 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, const SubPixel
     if (ps.kind != K_SPEC) ps.o = -ps.ray.d;
     ps.depth += 1;
     const double p = ps.depth <= (uint32_t)MAX_BOUNCES ? 1.0 : SURVIVAL_PROBABILITY;
-    Rng rng(a.seed, sp.pid, (uint32_t)smp, ps.depth, (uint32_t)sp.sub);
-    VertexDraws d;
+    Rng rng(ps.r0, ps.r1);
     if (obj.brdf == BRDF_SPECULAR) {
-        draw_vertex(rng, d, 3);
-        if (!(d.v[2] < p)) return false;
+        const bool survive = rng.uniform() < p;  // scene.rs:173
+        ps.r0 = rng.s0;
+        ps.r1 = rng.s1;
+        if (!survive) return false;
         V3 i;
         double pdf;
-        brdf_sample<C>(obj, nrm, ps.o, d, &i, &pdf);
+        brdf_sample<C>(obj, nrm, ps.o, rng, &i, &pdf);
         V3 f = brdf_eval<C>(obj, nrm, ps.o, i);
         ps.bemit = ps.beta;
         ps.beta = mult(ps.beta, f) * dot(nrm, i) / (pdf * p);
@@ -101,12 +105,11 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, const SubPixel
         ps.kind = K_SPEC;
         return true;
     }
-    draw_vertex(rng, d, (C::phong && obj.brdf == BRDF_PHONG) ? 6 : 5);
     const bool use_mis = C::mis && obj.brdf == BRDF_DIFFUSE;
     // next-event estimation (scene.rs:217-229)
     V3 y, ny;
     double pdfA;
-    light_sample<C>(sc, d, &y, &ny, &pdfA);
+    light_sample<C>(sc, rng, &y, &ny, &pdfA);
     V3 i = norm(y - x);
     double r_sqr = dot(y - x, y - x);
     V3 lef = mult(ld3(sc.objects[sc.light].emitted), brdf_eval<C>(obj, nrm, ps.o, i));
@@ -125,10 +128,12 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, const SubPixel
         ps.L = ps.L + mult(ps.beta, c);
     }
     // Russian roulette + BSDF continuation (scene.rs:231-240)
-    if (!(d.v[2] < p)) return false;
+    if (!(rng.uniform() < p)) return false;
     V3 wi;
     double pdf;
-    brdf_sample<C>(obj, nrm, ps.o, d, &wi, &pdf);
+    brdf_sample<C>(obj, nrm, ps.o, rng, &wi, &pdf);
+    ps.r0 = rng.s0;
+    ps.r1 = rng.s1;
     V3 f = brdf_eval<C>(obj, nrm, ps.o, wi);
     ps.beta = mult(ps.beta, f) * dot(nrm, wi) / (pdf * p);
     ps.ray = Ray{x, wi};

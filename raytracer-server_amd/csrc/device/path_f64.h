@@ -134,11 +134,15 @@ RT_DEV double div_x(double a, const Ray& r, const RayInv& v) { return v.fx ? qdi
 RT_DEV double div_y(double a, const Ray& r, const RayInv& v) { return v.fy ? qdiv(a, r.d.y, v.ry) : a / r.d.y; }
 RT_DEV double div_z(double a, const Ray& r, const RayInv& v) { return v.fz ? qdiv(a, r.d.z, v.rz) : a / r.d.z; }
 
-// ---------------------------------------------------------------- RNG
+// ---------------------------------------------------------------- RNG v2
+// One xoroshiro128++ stream per camera sample, seeded by Philox4x32-10(key = seed,
+// counter = (pixel, sample, 0, subpixel)); consumed in the reference's draw order along the path.
 struct Rng {
     uint64_t s0, s1;
-    RT_DEV Rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t depth, uint32_t sub) {
-        uint32_t c0 = pixel, c1 = sample, c2 = depth, c3 = sub;
+    RT_DEV Rng() : s0(1), s1(0) {}
+    RT_DEV Rng(uint64_t a, uint64_t b) : s0(a), s1(b) {}
+    RT_DEV Rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t sub) {
+        uint32_t c0 = pixel, c1 = sample, c2 = 0u, c3 = sub;
         uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
         for (int r = 0; r < 10; ++r) {
@@ -166,16 +170,6 @@ struct Rng {
     }
     RT_DEV double uniform() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
 };
-// Draw slots (fixed per vertex so every kernel consumes them identically):
-// camera (depth 0): r1, r2; vertex: light xi1, xi2, RR, bsdf u1, u2, u3, light pick.
-struct VertexDraws {
-    double v[7];
-};
-RT_DEV void draw_vertex(Rng& r, VertexDraws& d, int n) {
-#pragma unroll
-    for (int k = 0; k < 7; ++k)
-        if (k < n) d.v[k] = r.uniform();
-}
 
 // ---------------------------------------------------------------- primitives (geometry.rs:512-571)
 RT_DEV bool sphere_t(const DevObject& o, const Ray& ray, double* tout) {
@@ -296,64 +290,108 @@ RT_DEV bool leaf_hit(const DevScene& sc, int off, int cnt, const Ray& ray, doubl
     return any;
 }
 
-// Octree::intersect (geometry.rs:1237-1295), stackless: the per-ray child order (root-octant
-// centre distances, insertion-sorted, strict >) is identical at every level, so the DFS resumes
-// from parent links + the child's slot rank instead of a stack. Same visiting order and the same
-// first-leaf-with-a-hit exit as the reference recursion; no per-lane stack memory.
+// Octree::intersect (geometry.rs:1237-1295) as a flat per-lane state machine.
+// The reference visits children in an order fixed per ray (distances from the ray origin to the
+// ROOT box's octant centres, insertion-sorted with strict >, geometry.rs:1248-1260) and returns the
+// first subtree with any hit (leaf: nearest, strict <). The order is the same at every level, so
+// the DFS resumes from parent links + the child's rank instead of a stack. Each loop iteration does
+// exactly one box test or one triangle test per lane, so a divergent wave pays max(total steps)
+// rather than max(nodes) x max(children per node); empty octants are skipped with a permuted child
+// bitmask. Same visiting order, same early exit, same result bits.
+RT_DEV bool sqrt_gt(double a2, double b2) {
+    // sqrt(a2) > sqrt(b2) after rounding, without the square roots unless the radicands are within
+    // a few ulps (sqrt is monotone; a relative gap > 2^-50 survives both roundings).
+    if (!(a2 > b2)) return false;
+    if (a2 > b2 * (1.0 + 0x1p-50)) return true;
+    return sqrt(a2) > sqrt(b2);
+}
 RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double* t, int* prim) {
     if (m.n_nodes == 0) return false;
     if (!near_box(m.root_box, ray, inv, m.cull_pad)) return false;
     const int root = m.node_base;
     NodeMeta rm = sc.node_meta[root];
     if (rm.leaf_off >= 0) return leaf_hit(sc, rm.leaf_off, rm.leaf_cnt, ray, t, prim);
-    double dist[8];
+    // per-ray child order: insertion sort on (distance^2, octant) pairs held in registers
+    double d2[8];
+    int oc[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) dist[i] = mag(ld3(m.oct_center[i]) - ray.o);
-    uint32_t order = 0x76543210u;  // nibble k = octant visited k-th
+    for (int i = 0; i < 8; ++i) {
+        V3 dv = ld3(m.oct_center[i]) - ray.o;
+        d2[i] = dv.x * dv.x + dv.y * dv.y + dv.z * dv.z;  // mag()'s radicand, same operation order
+        oc[i] = i;
+    }
 #pragma unroll
     for (int i = 1; i < 8; ++i) {
 #pragma unroll
         for (int j = i; j > 0; --j) {
-            int a = (order >> (4 * (j - 1))) & 0xF, b = (order >> (4 * j)) & 0xF;
-            // insertion sort step (swap while strictly greater); unrolled as bubble passes with the
-            // same comparisons: stop condition emulated by the monotone prefix property.
-            if (dist[a] > dist[b]) {
-                order &= ~((0xFu << (4 * (j - 1))) | (0xFu << (4 * j)));
-                order |= ((uint32_t)b << (4 * (j - 1))) | ((uint32_t)a << (4 * j));
-            } else {
-                break;
-            }
+            // a sorted prefix has no inversion, so comparing past the insertion point swaps nothing:
+            // identical to the reference's early-exit loop
+            bool sw = sqrt_gt(d2[j - 1], d2[j]);
+            double td = d2[j - 1];
+            int to = oc[j - 1];
+            d2[j - 1] = sw ? d2[j] : td;
+            d2[j] = sw ? td : d2[j];
+            oc[j - 1] = sw ? oc[j] : to;
+            oc[j] = sw ? to : oc[j];
         }
     }
-    uint32_t rank = 0;  // nibble i = position of octant i in `order`
+    uint32_t order = 0, rank = 0;  // nibble k = octant visited k-th; nibble i = rank of octant i
 #pragma unroll
-    for (int k = 0; k < 8; ++k) rank |= (uint32_t)k << (4 * ((order >> (4 * k)) & 0xF));
-
-    int cur = root;
-    int k = 0;
+    for (int k = 0; k < 8; ++k) {
+        order |= (uint32_t)oc[k] << (4 * k);
+        rank |= (uint32_t)k << (4 * oc[k]);
+    }
+    int cur = root;        // current parent
+    uint32_t pm = 0;       // existing children of `cur`, permuted to visiting order
+    int k = 0;             // next rank to test at `cur`
+    int lpos = 0, lend = 0;  // leaf triangle cursor (lpos < lend: inside a leaf)
+    bool any = false, enter = true;
     while (true) {
-        int found = -1;
-        const int* ch = sc.node_child + 8 * (size_t)cur;
-        for (; k < 8; ++k) {
-            int oi = (order >> (4 * k)) & 0xF;
-            int c = ch[oi];
-            if (c >= 0 && box_hit(sc.node_box + 6 * (size_t)c, ray, inv)) { found = c; break; }
-        }
-        if (found >= 0) {
-            NodeMeta fm = sc.node_meta[found];
-            if (fm.leaf_off >= 0) {
-                if (leaf_hit(sc, fm.leaf_off, fm.leaf_cnt, ray, t, prim)) return true;
-                ++k;  // next sibling
-            } else {
-                cur = found;
-                k = 0;
+        if (lpos < lend) {
+            // one triangle test
+            int ti = sc.tri_ref[lpos];
+            double tt;
+            if (tri_t(sc.tris[ti], ray, &tt)) {
+                if (!any || tt < *t) { *t = tt; *prim = ti; any = true; }
+            }
+            if (++lpos == lend) {
+                if (any) return true;  // first leaf with a hit wins (geometry.rs:1267-1269)
+                ++k;
             }
             continue;
         }
-        if (cur == root) return false;
-        NodeMeta cm = sc.node_meta[cur];
-        k = (int)((rank >> (4 * cm.slot)) & 0xF) + 1;
-        cur = cm.parent;
+        if (enter) {  // build the permuted child mask of `cur`
+            const int* ch = sc.node_child + 8 * (size_t)cur;
+            pm = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) pm |= (uint32_t)(ch[(order >> (4 * q)) & 0xF] >= 0) << q;
+            enter = false;
+        }
+        const uint32_t rest = k < 8 ? (pm >> k) : 0u;
+        if (rest == 0u) {  // `cur` exhausted: resume at the parent, after cur's rank
+            if (cur == root) return false;
+            NodeMeta cm = sc.node_meta[cur];
+            k = (int)((rank >> (4 * cm.slot)) & 0xF) + 1;
+            cur = cm.parent;
+            enter = true;
+            continue;
+        }
+        k += __builtin_ctz(rest);
+        const int c = sc.node_child[8 * (size_t)cur + ((order >> (4 * k)) & 0xF)];
+        if (box_hit(sc.node_box + 6 * (size_t)c, ray, inv)) {
+            NodeMeta fm = sc.node_meta[c];
+            if (fm.leaf_off >= 0) {
+                lpos = fm.leaf_off;
+                lend = fm.leaf_off + fm.leaf_cnt;
+                if (lend == lpos) ++k;  // (empty leaves do not exist; defensive)
+            } else {
+                cur = c;
+                k = 0;
+                enter = true;
+            }
+        } else {
+            ++k;
+        }
     }
 }
 
@@ -534,11 +572,11 @@ RT_DEV void local_coord(V3 n, V3* u, V3* v, V3* w) {
 }
 // sample_incoming (scene.rs:56-98); draws: u1 = d[3], u2 = d[4], u3 = d[5].
 template <class C>
-RT_DEV void brdf_sample(const DevObject& o, V3 n, V3 out, const VertexDraws& d, V3* in, double* pdf) {
+RT_DEV void brdf_sample(const DevObject& o, V3 n, V3 out, Rng& rng, V3* in, double* pdf) {
     if (o.brdf == BRDF_DIFFUSE) {
-        double z = sqrt(d.v[3]);
+        double z = sqrt(rng.uniform());
         double r = sqrt(1.0 - z * z);
-        double phi = 2.0 * PI * d.v[4];
+        double phi = 2.0 * PI * rng.uniform();
         double sphi, cphi;
         sincos_2pi(phi, &sphi, &cphi);
         double x = r * cphi, y = r * sphi;
@@ -555,16 +593,16 @@ RT_DEV void brdf_sample(const DevObject& o, V3 n, V3 out, const VertexDraws& d, 
         return;
     }
     double p = (double)o.ph_power;
-    double u = d.v[3];
+    double u = rng.uniform();
     if (u < o.ph_kd) {
-        double xi1 = d.v[4], xi2 = d.v[5];
+        double xi1 = rng.uniform(), xi2 = rng.uniform();
         double sp, cp;
         sincos_2pi(2. * PI * xi2, &sp, &cp);
         V3 i = v3(sqrt(1. - xi1) * cp, sqrt(1. - xi1) * sp, sqrt(xi1));
         *in = i;
         *pdf = dot(n, i) * FRAC_1_PI;
     } else if (o.ph_kd <= u && u < o.ph_kd + o.ph_ks) {
-        double xi1 = d.v[4], xi2 = d.v[5];
+        double xi1 = rng.uniform(), xi2 = rng.uniform();
         double sp, cp;
         sincos_2pi(2. * PI * xi2, &sp, &cp);
         V3 i = v3(sqrt(1. - pow(xi1, 2. / (p + 1.))) * cp, sqrt(1. - pow(xi1, 2. / (p + 1.))) * sp,
@@ -579,10 +617,10 @@ RT_DEV void brdf_sample(const DevObject& o, V3 n, V3 out, const VertexDraws& d, 
 
 // ---------------------------------------------------------------- light (geometry.rs:573-595)
 template <class C>
-RT_DEV void light_sample(const DevScene& sc, const VertexDraws& d, V3* y, V3* ny, double* pdf) {
+RT_DEV void light_sample(const DevScene& sc, Rng& rng, V3* y, V3* ny, double* pdf) {
     const DevObject& L = sc.objects[sc.light];
     if (!C::mesh || L.geom == GEOM_SPHERE) {
-        double xi1 = d.v[0], xi2 = d.v[1];
+        double xi1 = rng.uniform(), xi2 = rng.uniform();
         double z = 2. * xi1 - 1.;
         double sp, cp;
         sincos_2pi(2. * PI * xi2, &sp, &cp);
@@ -596,7 +634,7 @@ RT_DEV void light_sample(const DevScene& sc, const VertexDraws& d, V3* y, V3* ny
     }
     // mesh light: area-weighted pick + Triangle::sample with the reference's missing `+ a`
     const DevMesh& m = sc.meshes[L.mesh];
-    double u = d.v[6] * m.total_weight;
+    double u = rng.uniform() * m.total_weight;
     int lo = 0, hi = m.n_tris - 1;  // first triangle whose cumulative area > u
     while (lo < hi) {
         int mid = (lo + hi) >> 1;
@@ -604,8 +642,8 @@ RT_DEV void light_sample(const DevScene& sc, const VertexDraws& d, V3* y, V3* ny
         else lo = mid + 1;
     }
     const DevTri& t = sc.tris[m.tri_base + lo];
-    double b0 = 1. - sqrt(d.v[0]);
-    double b1 = (1. - b0) * d.v[1];
+    double b0 = 1. - sqrt(rng.uniform());
+    double b1 = (1. - b0) * rng.uniform();
     V3 ab = norm(ld3(t.ab)), ac = norm(ld3(t.ac));
     *y = ab * b0 + ac * b1;
     *ny = ld3(t.n);

@@ -56,8 +56,8 @@ struct DevTri {
 // Compact per-type object tables, passed in the kernel arguments so the trace loops are unrolled
 // and their operands live in scalar registers (no per-object loads or type branches). Objects keep
 // their scene index for the reference's tie rule (scene.rs:278: ties go to the lower index).
-constexpr int kMaxAxisPlanes = 6;  // per axis
-constexpr int kMaxSpheres = 6;
+constexpr int kMaxAxisPlanes = 4;  // per axis
+constexpr int kMaxSpheres = 4;
 constexpr int kMaxGeneric = 8;     // meshes and non-axis planes
 
 struct DevScene {

@@ -23,6 +23,7 @@ struct PathStream {
     double* ex; double* ey; double* ez;   // throughput for the emission at the next hit (after a mirror)
     double* wx; double* wy; double* wz;   // the `o` argument carried across mirror bounces (scene.rs:178)
     double* pdf;                          // previous BSDF pdf (MIS only)
+    uint64_t* r0; uint64_t* r1;           // RNG stream state of the sample
     int32_t* sub;                         // tile-local subpixel id
     int32_t* sample;                      // sample index within the subpixel
     int32_t* dk;                          // depth << 2 | kind

@@ -37,6 +37,8 @@ RT_DEV void store_state(const PathStream& S, long i, const PathState& ps, int su
         S.wx[i] = ps.o.x; S.wy[i] = ps.o.y; S.wz[i] = ps.o.z;
     }
     if (mis) S.pdf[i] = ps.pdf_prev;
+    S.r0[i] = ps.r0;
+    S.r1[i] = ps.r1;
     S.sub[i] = sub;
     S.sample[i] = smp;
     S.dk[i] = (int32_t)((ps.depth << 2) | (uint32_t)ps.kind);
@@ -58,6 +60,8 @@ RT_DEV void load_state(const PathStream& S, long i, PathState& ps, int* sub, int
         ps.o = v3(0, 0, 0);
     }
     ps.pdf_prev = mis ? S.pdf[i] : 0.0;
+    ps.r0 = S.r0[i];
+    ps.r1 = S.r1[i];
     *sub = S.sub[i];
     *smp = S.sample[i];
 }
@@ -227,8 +231,8 @@ hipError_t Workspace::ensure_slots(size_t n) {
     if (blob) (void)hipFree(blob);
     blob = nullptr;
     slots = 0;
-    // per stream: 19 f64 arrays + 3 i32 arrays; hit: f64 + 2 i32
-    const size_t per_stream = n * (19 * sizeof(double) + 3 * sizeof(int32_t));
+    // per stream: 19 f64 arrays + 2 u64 + 3 i32 arrays; hit: f64 + 2 i32
+    const size_t per_stream = n * (21 * sizeof(double) + 3 * sizeof(int32_t));
     const size_t hits = n * (sizeof(double) + 2 * sizeof(int32_t));
     const size_t pad = 64 * 1024;
     e = hipMalloc(&blob, 2 * per_stream + hits + pad);
@@ -244,6 +248,8 @@ hipError_t Workspace::ensure_slots(size_t n) {
         double** f[] = {&S.ox, &S.oy, &S.oz, &S.dx, &S.dy, &S.dz, &S.bx, &S.by, &S.bz, &S.lx,
                         &S.ly, &S.lz, &S.ex, &S.ey, &S.ez, &S.wx, &S.wy, &S.wz, &S.pdf};
         for (double** q : f) *q = (double*)take(n * sizeof(double));
+        S.r0 = (uint64_t*)take(n * sizeof(uint64_t));
+        S.r1 = (uint64_t*)take(n * sizeof(uint64_t));
         S.sub = (int32_t*)take(n * sizeof(int32_t));
         S.sample = (int32_t*)take(n * sizeof(int32_t));
         S.dk = (int32_t*)take(n * sizeof(int32_t));

@@ -55,7 +55,7 @@ def lib():
         L.orc_octants.argtypes = [_D, _D, _D]
         L.orc_philox.argtypes = [_U32, _U32, _U32]
         L.orc_draws.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
-                                ctypes.c_uint32, ctypes.c_int, _D]
+                                ctypes.c_int, _D]
         L.orc_trace.argtypes = [ctypes.c_void_p, ctypes.c_int64, _D, _D, _D, _I32, _D, _D]
         L.orc_render.restype = ctypes.c_int64
         L.orc_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -220,7 +220,8 @@ def philox(ctr, key):
     return [int(x) for x in o]
 
 
-def draws(seed, pixel, sample, depth, sub, n=8):
+def draws(seed, pixel, sample, sub, n=8):
+    """First n uniforms of the stream of (pixel, sample, subpixel) — RNG spec v2."""
     out = np.zeros(n)
-    lib().orc_draws(seed, pixel, sample, depth, sub, n, _dp(out))
+    lib().orc_draws(seed, pixel, sample, sub, n, _dp(out))
     return out

@@ -34,11 +34,20 @@ def test_philox_known_answers(oracle):
 
 
 def test_draws_are_uniform_and_keyed(oracle):
-    a = np.array([oracle.draws(7, p, s, 3, 1, 5) for p in range(200) for s in range(20)])
+    a = np.array([oracle.draws(7, p, s, 1, 16) for p in range(200) for s in range(20)])
     assert a.min() >= 0.0 and a.max() < 1.0
     assert abs(a.mean() - 0.5) < 0.01 and abs(a.var() - 1 / 12) < 0.005
-    assert not np.array_equal(oracle.draws(7, 1, 2, 3, 0), oracle.draws(7, 1, 2, 3, 1))
-    assert np.array_equal(oracle.draws(7, 1, 2, 3, 0), oracle.draws(7, 1, 2, 3, 0))
+    # consecutive draws of one stream and draws of neighbouring streams are uncorrelated
+    assert abs(np.corrcoef(a[:, 0], a[:, 1])[0, 1]) < 0.05 and abs(np.corrcoef(a[:-1, 0], a[1:, 0])[0, 1]) < 0.05
+    assert not np.array_equal(oracle.draws(7, 1, 2, 0), oracle.draws(7, 1, 2, 1))
+    assert np.array_equal(oracle.draws(7, 1, 2, 0), oracle.draws(7, 1, 2, 0))
+    # stream seed = Philox4x32-10(key = seed, ctr = (pixel, sample, 0, sub)) -> xoroshiro128++ state
+    x = oracle.philox([5, 6, 0, 3], [7, 0])
+    s0, s1 = (x[0] << 32) | x[1], (x[2] << 32) | x[3]
+    M = (1 << 64) - 1
+    rotl = lambda v, k: ((v << k) | (v >> (64 - k))) & M
+    r = (rotl((s0 + s1) & M, 17) + s0) & M
+    assert oracle.draws(7, 5, 6, 3, 1)[0] == (r >> 11) * 2.0 ** -53
 
 
 def test_unicorn_octree_shape(oracle_scenes):
