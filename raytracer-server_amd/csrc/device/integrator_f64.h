@@ -69,7 +69,7 @@ RT_DEV void begin_sample(const DevScene& sc, const RenderArgs& a, const SubPixel
 // trace), false when this sample's radiance ps.L is final. The shadow ray of next-event estimation
 // is traced inline.
 template <class C>
-RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, const SubPixel& sp, int smp, PathState& ps,
+RT_DEV bool shade_vertex(const DevScene& sc, LdsTab* tab, const RenderArgs& a, const SubPixel& sp, int smp, PathState& ps,
                          const HitRec& hr) {
     if (hr.obj < 0) return false;  // no hit: R = 0 (scene.rs:157, :175, :233)
     const DevObject& obj = sc.objects[hr.obj];
@@ -114,7 +114,7 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, const SubPixel
     double r_sqr = dot(y - x, y - x);
     V3 lef = mult(ld3(sc.objects[sc.light].emitted), brdf_eval<C>(obj, nrm, ps.o, i));
     if (!is_zero(lef)) {  // a zero Le*f makes the term exactly 0: skip the shadow ray
-        double vis = visible<C>(sc, x, y) ? 1. : 0.;
+        double vis = visible<C>(sc, tab, x, y) ? 1. : 0.;
         V3 c;
         if (!use_mis) {
             c = lef * vis * dot(nrm, i) * dot(ny, -i) / (r_sqr * pdfA);

@@ -43,7 +43,7 @@ RT_DEV double qdiv(double a, double b, double y) {
     return r == 0.0 ? q0 : fma(r, y, q0);
 }
 RT_DEV V3 operator/(V3 a, double s) {
-    if (rcp_safe(s)) {
+    if (__all(rcp_safe(s))) {  // wave-uniform: no per-lane exec juggling on the common path
         double y = 1.0 / s;
         return v3(qdiv(a.x, s, y), qdiv(a.y, s, y), qdiv(a.z, s, y));
     }
@@ -115,24 +115,24 @@ struct Ray {
 RT_DEV V3 eval(const Ray& r, double t) { return r.o + t * r.d; }
 
 // Per-ray reciprocals of the direction for the divisions x / d.{x,y,z} (box faces, axis planes).
-// A component outside the safe range (0, tiny, huge, NaN) falls back to the IEEE division.
+// Bit-identical to the IEEE quotient whenever |d_k| is in [2^-900, 2^900]. Outside that range
+// (d_k = 0 or subnormal-tiny) the quotient becomes NaN/inf where the reference has +-inf or a
+// huge value; both only ever decide "this face/plane is not hit" (a plane needs |d_k| >= 1e-4; a
+// box face at t ~ 1/d_k lies far outside the box in the other coordinates for any direction with
+// |d| ~ 1), so the boolean outcomes are the reference's for every valid ray.
 struct RayInv {
     double rx, ry, rz;
-    bool fx, fy, fz;  // fast (Markstein) path usable
 };
 RT_DEV RayInv make_inv(const V3& d) {
     RayInv v;
-    v.fx = rcp_safe(d.x);
-    v.fy = rcp_safe(d.y);
-    v.fz = rcp_safe(d.z);
-    v.rx = v.fx ? 1.0 / d.x : 0.0;
-    v.ry = v.fy ? 1.0 / d.y : 0.0;
-    v.rz = v.fz ? 1.0 / d.z : 0.0;
+    v.rx = 1.0 / d.x;
+    v.ry = 1.0 / d.y;
+    v.rz = 1.0 / d.z;
     return v;
 }
-RT_DEV double div_x(double a, const Ray& r, const RayInv& v) { return v.fx ? qdiv(a, r.d.x, v.rx) : a / r.d.x; }
-RT_DEV double div_y(double a, const Ray& r, const RayInv& v) { return v.fy ? qdiv(a, r.d.y, v.ry) : a / r.d.y; }
-RT_DEV double div_z(double a, const Ray& r, const RayInv& v) { return v.fz ? qdiv(a, r.d.z, v.rz) : a / r.d.z; }
+RT_DEV double div_x(double a, const Ray& r, const RayInv& v) { return qdiv(a, r.d.x, v.rx); }
+RT_DEV double div_y(double a, const Ray& r, const RayInv& v) { return qdiv(a, r.d.y, v.ry); }
+RT_DEV double div_z(double a, const Ray& r, const RayInv& v) { return qdiv(a, r.d.z, v.rz); }
 
 // ---------------------------------------------------------------- RNG v2
 // One xoroshiro128++ stream per camera sample, seeded by Philox4x32-10(key = seed,
@@ -215,7 +215,7 @@ RT_DEV bool tri_t(const DevTri& tr, const Ray& ray, double* tout) {
     double det = det3(nd, ab, ac);
     double tn = det3(b, ab, ac), un = det3(nd, b, ac), vn = det3(nd, ab, b);
     double t, u, v;
-    if (rcp_safe(det)) {
+    if (__all(rcp_safe(det))) {  // wave-uniform
         double y = 1.0 / det;
         t = qdiv(tn, det, y);
         u = qdiv(un, det, y);
@@ -258,16 +258,13 @@ RT_DEV bool near_box(const double* bx, const Ray& r, const RayInv& inv, double p
     double t0 = 0.0, t1 = INFINITY;
     const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
     const double rc[3] = {inv.rx, inv.ry, inv.rz};
-    const bool f[3] = {inv.fx, inv.fy, inv.fz};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         double lo = bx[k] - pad, hi = bx[3 + k] + pad;
-        if (!f[k]) {
-            if (fabs(d[k]) < 0x1p-900) {  // (nearly) parallel slab: origin must lie inside it
-                if (o[k] < lo || o[k] > hi) return false;
-                continue;
-            }
-            return true;  // NaN / huge: do not cull
+        if (!(fabs(d[k]) >= 0x1p-900 && fabs(d[k]) <= 0x1p900)) {
+            if (!(fabs(d[k]) < 0x1p-900)) return true;  // NaN / huge: do not cull
+            if (o[k] < lo || o[k] > hi) return false;  // (nearly) parallel slab: origin must lie inside it
+            continue;
         }
         double ta = (lo - o[k]) * rc[k], tb = (hi - o[k]) * rc[k];
         double tn = fmin(ta, tb), tf = fmax(ta, tb);
@@ -405,6 +402,24 @@ struct Cfg {
     static constexpr bool compact = (F & 8) != 0;  // scene fits the compact tables (DevScene)
 };
 
+// Copies the compact tables (axis-plane coordinates, sphere centres and r^2) into LDS once per
+// workgroup: the trace loops then read them with broadcast ds_reads instead of holding ~56 SGPRs
+// (which spilled, and were restored with v_readlane bursts in every plane test).
+template <class C>
+RT_DEV LdsTab* stage_tables(const DevScene& sc, double* lds) {
+    if constexpr (C::compact) {
+        const int tid = threadIdx.x;
+        if (tid < kTabSize) {
+            double v;
+            if (tid < kTabSph) v = sc.ax_pos[tid / kMaxAxisPlanes][tid % kMaxAxisPlanes];
+            else v = sc.sph[(tid - kTabSph) / 4][(tid - kTabSph) % 4];
+            lds[tid] = v;
+        }
+        __syncthreads();
+    }
+    return (LdsTab*)lds;
+}
+
 // One object's Geometry::intersect, reporting t (and the triangle for meshes).
 template <class C>
 RT_DEV bool object_t(const DevScene& sc, const DevObject& o, const Ray& ray, const RayInv& inv, double* t, int* prim) {
@@ -425,7 +440,7 @@ RT_DEV void consider(HitRec& h, double t, int idx, int prim) {
     if (h.obj < 0 || t < h.t || (t == h.t && idx < h.obj)) { h.t = t; h.obj = idx; h.prim = prim; }
 }
 // Sphere test on the compact table (same operations as sphere_t; r*r precomputed exactly).
-RT_DEV bool sphere_c(const double* c, const Ray& ray, double* tout) {
+RT_DEV bool sphere_c(LdsTab* c, const Ray& ray, double* tout) {
     V3 op = v3(c[0], c[1], c[2]) - ray.o;
     double b = dot(op, ray.d);
     double det = b * b - dot(op, op) + c[3];
@@ -439,7 +454,7 @@ RT_DEV bool sphere_c(const double* c, const Ray& ray, double* tout) {
 }
 // Axis planes of axis K: one |d_K| test and one reciprocal serve all of them (plane_t's axis path).
 template <int K, class Visit>
-RT_DEV void axis_planes(const DevScene& sc, const Ray& ray, const RayInv& inv, Visit&& visit) {
+RT_DEV void axis_planes(const DevScene& sc, LdsTab* tab, const Ray& ray, const RayInv& inv, Visit&& visit) {
     const int n = sc.n_ax[K];
     if (n == 0) return;
     const double dk = K == 0 ? ray.d.x : K == 1 ? ray.d.y : ray.d.z;
@@ -448,7 +463,7 @@ RT_DEV void axis_planes(const DevScene& sc, const Ray& ray, const RayInv& inv, V
 #pragma unroll
     for (int i = 0; i < kMaxAxisPlanes; ++i) {
         if (i < n) {
-            double num = sc.ax_pos[K][i] - ok;
+            double num = tab[K * kMaxAxisPlanes + i] - ok;
             double t = K == 0 ? div_x(num, ray, inv) : K == 1 ? div_y(num, ray, inv) : div_z(num, ray, inv);
             if (t >= 0.) visit(t, sc.ax_idx[K][i], -1);
         }
@@ -456,18 +471,18 @@ RT_DEV void axis_planes(const DevScene& sc, const Ray& ray, const RayInv& inv, V
 }
 
 template <class C>
-RT_DEV HitRec trace_closest(const DevScene& sc, const Ray& ray) {
+RT_DEV HitRec trace_closest(const DevScene& sc, LdsTab* tab, const Ray& ray) {
     HitRec h{0.0, -1, -1};
     const RayInv inv = make_inv(ray.d);
     if constexpr (C::compact) {
         auto visit = [&](double t, int idx, int prim) { consider(h, t, idx, prim); };
-        axis_planes<0>(sc, ray, inv, visit);
-        axis_planes<1>(sc, ray, inv, visit);
-        axis_planes<2>(sc, ray, inv, visit);
+        axis_planes<0>(sc, tab, ray, inv, visit);
+        axis_planes<1>(sc, tab, ray, inv, visit);
+        axis_planes<2>(sc, tab, ray, inv, visit);
 #pragma unroll
         for (int i = 0; i < kMaxSpheres; ++i) {
             double t;
-            if (i < sc.n_sph && sphere_c(sc.sph[i], ray, &t)) consider(h, t, sc.sph_idx[i], -1);
+            if (i < sc.n_sph && sphere_c(tab + kTabSph + 4 * i, ray, &t)) consider(h, t, sc.sph_idx[i], -1);
         }
         for (int i = 0; i < sc.n_gen; ++i) {
             const int idx = sc.gen_idx[i];
@@ -514,7 +529,7 @@ RT_DEV void surface(const DevScene& sc, const Ray& ray, const HitRec& h, V3* pos
 // intersect t satisfies t + 0.001 < |y - x| (equivalent to the nearest-hit test because x + 0.001
 // rounds monotonically). Analytic objects are tested before meshes (order-free for a boolean).
 template <class C>
-RT_DEV bool visible(const DevScene& sc, V3 x, V3 y) {
+RT_DEV bool visible(const DevScene& sc, LdsTab* tab, V3 x, V3 y) {
     const double ERR_MARGIN = 0.001;
     V3 diff = y - x;
     double dist = mag(diff);
@@ -523,13 +538,13 @@ RT_DEV bool visible(const DevScene& sc, V3 x, V3 y) {
     if constexpr (C::compact) {
         bool occluded = false;
         auto visit = [&](double t, int, int) { occluded |= !(t + ERR_MARGIN >= dist); };
-        axis_planes<0>(sc, r, inv, visit);
-        axis_planes<1>(sc, r, inv, visit);
-        axis_planes<2>(sc, r, inv, visit);
+        axis_planes<0>(sc, tab, r, inv, visit);
+        axis_planes<1>(sc, tab, r, inv, visit);
+        axis_planes<2>(sc, tab, r, inv, visit);
 #pragma unroll
         for (int i = 0; i < kMaxSpheres; ++i) {
             double t;
-            if (i < sc.n_sph && sphere_c(sc.sph[i], r, &t)) occluded |= !(t + ERR_MARGIN >= dist);
+            if (i < sc.n_sph && sphere_c(tab + kTabSph + 4 * i, r, &t)) occluded |= !(t + ERR_MARGIN >= dist);
         }
         if (occluded) return false;
         for (int i = 0; i < sc.n_gen; ++i) {

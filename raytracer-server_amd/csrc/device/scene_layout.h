@@ -59,6 +59,8 @@ struct DevTri {
 constexpr int kMaxAxisPlanes = 4;  // per axis
 constexpr int kMaxSpheres = 4;
 constexpr int kMaxGeneric = 8;     // meshes and non-axis planes
+constexpr int kTabSph = 3 * kMaxAxisPlanes;          // LDS table: axis-plane coordinates, then
+constexpr int kTabSize = kTabSph + 4 * kMaxSpheres;  //   sphere (centre xyz, r^2)
 
 struct DevScene {
     const DevObject* objects;
@@ -81,5 +83,9 @@ struct DevScene {
     double sph[kMaxSpheres][4];              // centre xyz, r*r
     int32_t gen_idx[kMaxGeneric];            // everything else, through the generic intersector
 };
+
+// LDS-resident copy of the compact tables (ax_pos, then sph), typed in the LDS address space so
+// reads compile to ds_read (a generic pointer would become flat_load).
+typedef const __attribute__((address_space(3))) double LdsTab;
 
 }  // namespace rt

@@ -38,6 +38,8 @@ template <int F, int W>
 __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
                                                           uint32_t* next_sub, long nsub) {
     using C = Cfg<F>;
+    __shared__ double s_tab[kTabSize];
+    LdsTab* tab = stage_tables<C>(sc, s_tab);
     const int lane = threadIdx.x & 63;
     unsigned long long nverts = 0;
     long id = wave_ticket(next_sub, true);
@@ -51,9 +53,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
         bool done = false;
         if (active) {
             if (fresh) begin_sample(sc, a, sp, s, ps);
-            HitRec hr = trace_closest<C>(sc, ps.ray);
+            HitRec hr = trace_closest<C>(sc, tab, ps.ray);
             nverts += hr.obj >= 0;
-            fresh = !shade_vertex<C>(sc, a, sp, s, ps, hr);
+            fresh = !shade_vertex<C>(sc, tab, a, sp, s, ps, hr);
             if (fresh) {
                 acc = acc + ps.L * a.inv_n;  // server.rs:357-358
                 if (++s == a.n_samples) {
@@ -104,10 +106,12 @@ __global__ __launch_bounds__(256) void k_finalize_f64(RenderArgs a, const double
 __global__ __launch_bounds__(256) void k_trace_f64(DevScene sc, long n, const double* __restrict__ o,
                                                    const double* __restrict__ d, double* t, int32_t* obj,
                                                    double* pos, double* nrm) {
+    __shared__ double s_tab[kTabSize];
+    LdsTab* tab = stage_tables<Cfg<9>>(sc, s_tab);
     long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Ray r{v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2])};
-    HitRec h = trace_closest<Cfg<1>>(sc, r);
+    HitRec h = sc.compact ? trace_closest<Cfg<9>>(sc, tab, r) : trace_closest<Cfg<1>>(sc, tab, r);
     obj[i] = h.obj;
     t[i] = h.obj >= 0 ? h.t : 0.0;
     if (h.obj >= 0) {

@@ -101,12 +101,14 @@ template <int F>
 __global__ __launch_bounds__(kBlock) void k_wf_extend(DevScene sc, PathStream A, const uint32_t* cnt_in,
                                                        uint32_t* cnt_out, double* __restrict__ ht,
                                                        int32_t* __restrict__ hobj, int32_t* __restrict__ hprim) {
+    __shared__ double s_tab[kTabSize];
+    LdsTab* tab = stage_tables<Cfg<F>>(sc, s_tab);
     const long n = (long)*cnt_in;
     if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_out = 0;  // stream B is refilled by k_wf_shade
     const long stride = (long)gridDim.x * blockDim.x;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         Ray r{v3(A.ox[i], A.oy[i], A.oz[i]), v3(A.dx[i], A.dy[i], A.dz[i])};
-        HitRec h = trace_closest<Cfg<F>>(sc, r);
+        HitRec h = trace_closest<Cfg<F>>(sc, tab, r);
         ht[i] = h.t;
         hobj[i] = h.obj;
         hprim[i] = h.prim;
@@ -120,6 +122,8 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, 
                                                       const int32_t* __restrict__ hobj,
                                                       const int32_t* __restrict__ hprim, double* sub_buf,
                                                       unsigned long long* counters) {
+    __shared__ double s_tab[kTabSize];
+    LdsTab* tab = stage_tables<Cfg<F>>(sc, s_tab);
     const long n = (long)*cnt_in;
     const long stride = (long)gridDim.x * blockDim.x;
     const bool mis = a.mis != 0;
@@ -136,7 +140,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, 
             HitRec hr{ht[i], hobj[i], hprim[i]};
             nverts += hr.obj >= 0;
             SubPixel sp = subpixel_of(a, sub);
-            emit = shade_vertex<Cfg<F>>(sc, a, sp, smp, ps, hr);
+            emit = shade_vertex<Cfg<F>>(sc, tab, a, sp, smp, ps, hr);
             if (!emit) {
                 // sample finished: sequential mean update (server.rs:357-358), then regenerate
                 double* acc = sub_buf + (size_t)sub * 3;
