@@ -20,6 +20,7 @@ struct RenderArgs {
     double* sub_out;      // optional [pix][4][3]
     uint8_t* rgb_out;     // [pix][3]
     unsigned long long* counters;  // optional [0] = path vertices
+    const int32_t* cancel;         // optional device view of the host cancel flag (mapped memory)
 };
 
 hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,

@@ -67,9 +67,13 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
                 }
             }
         }
-        long nid = wave_ticket(next_sub, done);
+        // cancellation (RenderJob::stop, server.rs:201-203): checked when a lane would start a new
+        // subpixel; a set flag stops handing out work, lanes finish the subpixel they hold
+        bool stop = false;
+        if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+        long nid = wave_ticket(next_sub, done && !stop);
         if (done) {
-            id = nid;
+            id = stop ? nsub : nid;
             active = id < nsub;
             if (active) sp = subpixel_of(a, id);
             acc = v3(0, 0, 0);

@@ -323,6 +323,18 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
     std::string err;
     if (p->flags & RT_FLAG_MEGAKERNEL) {
         const size_t npix = (size_t)p->tile_w * p->tile_h;
+        // device view of the caller's cancel flag: the megakernel polls it between subpixels
+        void* dcancel = nullptr;
+        bool registered = false;
+        if (cancel) {
+            hipError_t er = hipHostRegister((void*)cancel, sizeof(int32_t), hipHostRegisterMapped);
+            registered = er == hipSuccess;
+            if (er == hipSuccess || er == hipErrorHostMemoryAlreadyRegistered) {
+                if (hipHostGetDevicePointer(&dcancel, (void*)cancel, 0) != hipSuccess) dcancel = nullptr;
+            }
+            (void)hipGetLastError();
+        }
+        a.cancel = (const int32_t*)dcancel;
         hipError_t e = ws->ensure_counters();
         double* sub = d_sub;
         if (e == hipSuccess && !sub) {
@@ -337,6 +349,13 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
         }
         if (e == hipSuccess) e = rt::launch_finalize_f64(a, sub, st);
         if (e != hipSuccess) { out = RT_E_HIP; err = std::string("megakernel: ") + hipGetErrorString(e); }
+        if (cancel) {
+            // the flag must stay registered until the kernel that polls it has finished
+            hipError_t es = hipStreamSynchronize(st);
+            if (es != hipSuccess && out == RT_OK) { out = RT_E_HIP; err = std::string("megakernel: ") + hipGetErrorString(es); }
+            if (registered) (void)hipHostUnregister((void*)cancel);
+            if (out == RT_OK && *cancel) out = RT_CANCELLED;
+        }
     } else {
         out = rt::wavefront_render_f64(ds, a, *ws, st, cancel, stats, &err);
     }

@@ -155,3 +155,20 @@ def test_mis_parity_small(rt, gpu_scenes, oracle_scenes):
     rgb_g, sub_g, st, rgb_o, sub_o, st_o = _render_pair(rt, gpu_scenes["cornell_box"], oracle_scenes["cornell_box"],
                                                         64, 48, 16, mis=True)
     _assert_parity(rgb_g, sub_g, rgb_o, sub_o, "cornell/mis")
+
+
+@pytest.mark.parametrize("megakernel", [True, False], ids=["megakernel", "wavefront"])
+def test_cancel(rt, gpu_scenes, megakernel):
+    """RenderJob::stop semantics (server.rs:201-203): a set flag ends a long render early."""
+    import ctypes
+    import threading
+    import time
+
+    flag = ctypes.c_int32(0)
+    timer = threading.Timer(0.3, lambda: setattr(flag, "value", 1))
+    t0 = time.time()
+    timer.start()
+    _, _, st = rt.render(gpu_scenes["cornell_box"], 1920, 1080, 4096, SEED, megakernel=megakernel, cancel=flag)
+    dt = time.time() - t0
+    timer.cancel()
+    assert st["cancelled"] and dt < 4.0, (st["cancelled"], dt)
