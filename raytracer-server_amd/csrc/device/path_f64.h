@@ -287,6 +287,79 @@ RT_DEV bool leaf_hit(const DevScene& sc, int off, int cnt, const Ray& ray, doubl
     return any;
 }
 
+// shared by both traversals
+RT_DEV bool sqrt_gt(double a2, double b2) {
+    // sqrt(a2) > sqrt(b2) after rounding, without the square roots unless the radicands are within
+    // a few ulps (sqrt is monotone; a relative gap > 2^-50 survives both roundings).
+    if (!(a2 > b2)) return false;
+    if (a2 > b2 * (1.0 + 0x1p-50)) return true;
+    return sqrt(a2) > sqrt(b2);
+}
+#if !RT_TRAVERSAL_FLAT
+// Octree::intersect (geometry.rs:1237-1295), stackless (default traversal): the per-ray child order (root-octant
+// centre distances, insertion-sorted, strict >) is identical at every level, so the DFS resumes
+// from parent links + the child's slot rank instead of a stack. Same visiting order and the same
+// first-leaf-with-a-hit exit as the reference recursion; no per-lane stack memory.
+RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double* t, int* prim) {
+    if (m.n_nodes == 0) return false;
+    if (!near_box(m.root_box, ray, inv, m.cull_pad)) return false;
+    const int root = m.node_base;
+    NodeMeta rm = sc.node_meta[root];
+    if (rm.leaf_off >= 0) return leaf_hit(sc, rm.leaf_off, rm.leaf_cnt, ray, t, prim);
+    double d2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        V3 dv = ld3(m.oct_center[i]) - ray.o;
+        d2[i] = dv.x * dv.x + dv.y * dv.y + dv.z * dv.z;  // mag()'s radicand, same operation order
+    }
+    uint32_t order = 0x76543210u;  // nibble k = octant visited k-th
+#pragma unroll
+    for (int i = 1; i < 8; ++i) {
+#pragma unroll
+        for (int j = i; j > 0; --j) {
+            // insertion sort step (swap while strictly greater, geometry.rs:1251-1260)
+            int a = (order >> (4 * (j - 1))) & 0xF, b = (order >> (4 * j)) & 0xF;
+            if (sqrt_gt(d2[a], d2[b])) {
+                order &= ~((0xFu << (4 * (j - 1))) | (0xFu << (4 * j)));
+                order |= ((uint32_t)b << (4 * (j - 1))) | ((uint32_t)a << (4 * j));
+            } else {
+                break;
+            }
+        }
+    }
+    uint32_t rank = 0;  // nibble i = position of octant i in `order`
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rank |= (uint32_t)k << (4 * ((order >> (4 * k)) & 0xF));
+
+    int cur = root;
+    int k = 0;
+    while (true) {
+        int found = -1;
+        const int* ch = sc.node_child + 8 * (size_t)cur;
+        for (; k < 8; ++k) {
+            int oi = (order >> (4 * k)) & 0xF;
+            int c = ch[oi];
+            if (c >= 0 && box_hit(sc.node_box + 6 * (size_t)c, ray, inv)) { found = c; break; }
+        }
+        if (found >= 0) {
+            NodeMeta fm = sc.node_meta[found];
+            if (fm.leaf_off >= 0) {
+                if (leaf_hit(sc, fm.leaf_off, fm.leaf_cnt, ray, t, prim)) return true;
+                ++k;  // next sibling
+            } else {
+                cur = found;
+                k = 0;
+            }
+            continue;
+        }
+        if (cur == root) return false;
+        NodeMeta cm = sc.node_meta[cur];
+        k = (int)((rank >> (4 * cm.slot)) & 0xF) + 1;
+        cur = cm.parent;
+    }
+}
+
+#else
 // Octree::intersect (geometry.rs:1237-1295) as a flat per-lane state machine.
 // The reference visits children in an order fixed per ray (distances from the ray origin to the
 // ROOT box's octant centres, insertion-sorted with strict >, geometry.rs:1248-1260) and returns the
@@ -295,13 +368,6 @@ RT_DEV bool leaf_hit(const DevScene& sc, int off, int cnt, const Ray& ray, doubl
 // exactly one box test or one triangle test per lane, so a divergent wave pays max(total steps)
 // rather than max(nodes) x max(children per node); empty octants are skipped with a permuted child
 // bitmask. Same visiting order, same early exit, same result bits.
-RT_DEV bool sqrt_gt(double a2, double b2) {
-    // sqrt(a2) > sqrt(b2) after rounding, without the square roots unless the radicands are within
-    // a few ulps (sqrt is monotone; a relative gap > 2^-50 survives both roundings).
-    if (!(a2 > b2)) return false;
-    if (a2 > b2 * (1.0 + 0x1p-50)) return true;
-    return sqrt(a2) > sqrt(b2);
-}
 RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double* t, int* prim) {
     if (m.n_nodes == 0) return false;
     if (!near_box(m.root_box, ray, inv, m.cull_pad)) return false;
@@ -392,6 +458,8 @@ RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const
     }
 }
 
+#endif  // RT_TRAVERSAL_FLAT
+
 // Kernel specialisation by scene features (chosen on the host per scene/flags): code paths a
 // scene cannot reach are not compiled into its kernels, which keeps register pressure down.
 template <int F>
@@ -405,9 +473,21 @@ struct Cfg {
 // Copies the compact tables (axis-plane coordinates, sphere centres and r^2) into LDS once per
 // workgroup: the trace loops then read them with broadcast ds_reads instead of holding ~56 SGPRs
 // (which spilled, and were restored with v_readlane bursts in every plane test).
+// RT_LDS_TABLES=1 reads the compact tables from LDS; the default keeps them in kernel arguments
+// (scalar registers), measured 26% faster on cornell_box (profiles/r01_variants.log).
+#ifndef RT_LDS_TABLES
+#define RT_LDS_TABLES 0
+#endif
+#if RT_LDS_TABLES
+#define RT_TAB_AX(K, i) tab[(K) * kMaxAxisPlanes + (i)]
+#define RT_TAB_SPH(i) (tab + kTabSph + 4 * (i))
+#else
+#define RT_TAB_AX(K, i) sc.ax_pos[K][i]
+#define RT_TAB_SPH(i) (sc.sph[i])
+#endif
 template <class C>
 RT_DEV LdsTab* stage_tables(const DevScene& sc, double* lds) {
-    if constexpr (C::compact) {
+    if constexpr (C::compact && RT_LDS_TABLES) {
         const int tid = threadIdx.x;
         if (tid < kTabSize) {
             double v;
@@ -440,7 +520,8 @@ RT_DEV void consider(HitRec& h, double t, int idx, int prim) {
     if (h.obj < 0 || t < h.t || (t == h.t && idx < h.obj)) { h.t = t; h.obj = idx; h.prim = prim; }
 }
 // Sphere test on the compact table (same operations as sphere_t; r*r precomputed exactly).
-RT_DEV bool sphere_c(LdsTab* c, const Ray& ray, double* tout) {
+template <class P>
+RT_DEV bool sphere_c(P c, const Ray& ray, double* tout) {
     V3 op = v3(c[0], c[1], c[2]) - ray.o;
     double b = dot(op, ray.d);
     double det = b * b - dot(op, op) + c[3];
@@ -463,7 +544,7 @@ RT_DEV void axis_planes(const DevScene& sc, LdsTab* tab, const Ray& ray, const R
 #pragma unroll
     for (int i = 0; i < kMaxAxisPlanes; ++i) {
         if (i < n) {
-            double num = tab[K * kMaxAxisPlanes + i] - ok;
+            double num = RT_TAB_AX(K, i) - ok;
             double t = K == 0 ? div_x(num, ray, inv) : K == 1 ? div_y(num, ray, inv) : div_z(num, ray, inv);
             if (t >= 0.) visit(t, sc.ax_idx[K][i], -1);
         }
@@ -482,7 +563,7 @@ RT_DEV HitRec trace_closest(const DevScene& sc, LdsTab* tab, const Ray& ray) {
 #pragma unroll
         for (int i = 0; i < kMaxSpheres; ++i) {
             double t;
-            if (i < sc.n_sph && sphere_c(tab + kTabSph + 4 * i, ray, &t)) consider(h, t, sc.sph_idx[i], -1);
+            if (i < sc.n_sph && sphere_c(RT_TAB_SPH(i), ray, &t)) consider(h, t, sc.sph_idx[i], -1);
         }
         for (int i = 0; i < sc.n_gen; ++i) {
             const int idx = sc.gen_idx[i];
@@ -544,7 +625,7 @@ RT_DEV bool visible(const DevScene& sc, LdsTab* tab, V3 x, V3 y) {
 #pragma unroll
         for (int i = 0; i < kMaxSpheres; ++i) {
             double t;
-            if (i < sc.n_sph && sphere_c(tab + kTabSph + 4 * i, r, &t)) occluded |= !(t + ERR_MARGIN >= dist);
+            if (i < sc.n_sph && sphere_c(RT_TAB_SPH(i), r, &t)) occluded |= !(t + ERR_MARGIN >= dist);
         }
         if (occluded) return false;
         for (int i = 0; i < sc.n_gen; ++i) {

@@ -17,7 +17,7 @@ import struct
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librtamd.so")
+LIB_PATH = os.environ.get("RT_AMD_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "librtamd.so")
 
 RT_OK = 0
 RT_CANCELLED = 1
