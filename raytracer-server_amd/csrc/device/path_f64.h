@@ -254,7 +254,10 @@ RT_DEV bool box_hit(const double* bx, const Ray& r, const RayInv& inv) {
 // Conservative cull: false only if the ray (t >= 0) passes farther than `pad` from the box, in
 // which case no box contained in it can pass box_hit (its face points would be within rounding,
 // ~1e-11, of the ray). Exactness argument in DESIGN.md §Octree.
-RT_DEV bool near_box(const double* bx, const Ray& r, const RayInv& inv, double pad) {
+// tmax: the caller's bound on a useful hit (closest analytic hit so far, or the shadow distance);
+// every mesh hit point lies in the mesh's bbox (the octree root box encloses all its triangles), so
+// a box entered only beyond tmax (with margin) cannot produce a hit that would be used.
+RT_DEV bool near_box(const double* bx, const Ray& r, const RayInv& inv, double pad, double tmax) {
     double t0 = 0.0, t1 = INFINITY;
     const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
     const double rc[3] = {inv.rx, inv.ry, inv.rz};
@@ -271,8 +274,16 @@ RT_DEV bool near_box(const double* bx, const Ray& r, const RayInv& inv, double p
         t0 = fmax(t0, tn - 1e-9 * fabs(tn));
         t1 = fmin(t1, tf + 1e-9 * fabs(tf));
     }
-    return t0 <= t1;
+    return t0 <= t1 && t0 <= tmax * (1.0 + 1e-9) + 1e-9;
 }
+
+// Diagnostic build only (make EXTRA=-DRT_DEBUG_COUNTERS=1): traversal work counters.
+#if RT_DEBUG_COUNTERS
+__device__ unsigned long long g_dbg[8];  // 0 mesh calls, 1 past cull, 2 node visits, 3 box tests, 4 tri tests
+#define RT_DBG(i) atomicAdd(&g_dbg[i], 1ull)
+#else
+#define RT_DBG(i) ((void)0)
+#endif
 
 // Leaf: nearest triangle, strict < (geometry.rs:1276-1293).
 RT_DEV bool leaf_hit(const DevScene& sc, int off, int cnt, const Ray& ray, double* t, int* prim) {
@@ -280,6 +291,7 @@ RT_DEV bool leaf_hit(const DevScene& sc, int off, int cnt, const Ray& ray, doubl
     for (int r = 0; r < cnt; ++r) {
         int ti = sc.tri_ref[off + r];
         double tt;
+        RT_DBG(4);
         if (tri_t(sc.tris[ti], ray, &tt)) {
             if (!any || tt < *t) { *t = tt; *prim = ti; any = true; }
         }
@@ -300,9 +312,12 @@ RT_DEV bool sqrt_gt(double a2, double b2) {
 // centre distances, insertion-sorted, strict >) is identical at every level, so the DFS resumes
 // from parent links + the child's slot rank instead of a stack. Same visiting order and the same
 // first-leaf-with-a-hit exit as the reference recursion; no per-lane stack memory.
-RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double* t, int* prim) {
+RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax, double* t,
+                     int* prim) {
     if (m.n_nodes == 0) return false;
-    if (!near_box(m.root_box, ray, inv, m.cull_pad)) return false;
+    RT_DBG(0);
+    if (!near_box(m.root_box, ray, inv, m.cull_pad, tmax)) return false;
+    RT_DBG(1);
     const int root = m.node_base;
     NodeMeta rm = sc.node_meta[root];
     if (rm.leaf_off >= 0) return leaf_hit(sc, rm.leaf_off, rm.leaf_cnt, ray, t, prim);
@@ -335,10 +350,12 @@ RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const
     int k = 0;
     while (true) {
         int found = -1;
+        RT_DBG(2);
         const int* ch = sc.node_child + 8 * (size_t)cur;
         for (; k < 8; ++k) {
             int oi = (order >> (4 * k)) & 0xF;
             int c = ch[oi];
+            if (c >= 0) RT_DBG(3);
             if (c >= 0 && box_hit(sc.node_box + 6 * (size_t)c, ray, inv)) { found = c; break; }
         }
         if (found >= 0) {
@@ -368,9 +385,10 @@ RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const
 // exactly one box test or one triangle test per lane, so a divergent wave pays max(total steps)
 // rather than max(nodes) x max(children per node); empty octants are skipped with a permuted child
 // bitmask. Same visiting order, same early exit, same result bits.
-RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double* t, int* prim) {
+RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax, double* t,
+                     int* prim) {
     if (m.n_nodes == 0) return false;
-    if (!near_box(m.root_box, ray, inv, m.cull_pad)) return false;
+    if (!near_box(m.root_box, ray, inv, m.cull_pad, tmax)) return false;
     const int root = m.node_base;
     NodeMeta rm = sc.node_meta[root];
     if (rm.leaf_off >= 0) return leaf_hit(sc, rm.leaf_off, rm.leaf_cnt, ray, t, prim);
@@ -502,10 +520,11 @@ RT_DEV LdsTab* stage_tables(const DevScene& sc, double* lds) {
 
 // One object's Geometry::intersect, reporting t (and the triangle for meshes).
 template <class C>
-RT_DEV bool object_t(const DevScene& sc, const DevObject& o, const Ray& ray, const RayInv& inv, double* t, int* prim) {
+RT_DEV bool object_t(const DevScene& sc, const DevObject& o, const Ray& ray, const RayInv& inv, double* t, int* prim,
+                     double tmax = INFINITY) {
     if (o.geom == GEOM_SPHERE) return sphere_t(o, ray, t);
     if (o.geom == GEOM_PLANE) return plane_t(o, ray, inv, t);
-    if constexpr (C::mesh) return mesh_hit(sc, sc.meshes[o.mesh], ray, inv, t, prim);
+    if constexpr (C::mesh) return mesh_hit(sc, sc.meshes[o.mesh], ray, inv, tmax, t, prim);
     return false;
 }
 
@@ -569,7 +588,8 @@ RT_DEV HitRec trace_closest(const DevScene& sc, LdsTab* tab, const Ray& ray) {
             const int idx = sc.gen_idx[i];
             double t;
             int prim = -1;
-            if (object_t<C>(sc, sc.objects[idx], ray, inv, &t, &prim)) consider(h, t, idx, prim);
+            const double tmax = h.obj >= 0 ? h.t : INFINITY;
+            if (object_t<C>(sc, sc.objects[idx], ray, inv, &t, &prim, tmax)) consider(h, t, idx, prim);
         }
         return h;
     }
@@ -631,7 +651,8 @@ RT_DEV bool visible(const DevScene& sc, LdsTab* tab, V3 x, V3 y) {
         for (int i = 0; i < sc.n_gen; ++i) {
             double t;
             int prim;
-            if (object_t<C>(sc, sc.objects[sc.gen_idx[i]], r, inv, &t, &prim) && !(t + ERR_MARGIN >= dist)) return false;
+            if (object_t<C>(sc, sc.objects[sc.gen_idx[i]], r, inv, &t, &prim, dist) && !(t + ERR_MARGIN >= dist))
+                return false;
         }
         return true;
     }
@@ -641,7 +662,7 @@ RT_DEV bool visible(const DevScene& sc, LdsTab* tab, V3 x, V3 y) {
             if ((o.geom == GEOM_MESH) != (pass == 1)) continue;
             double t;
             int prim;
-            if (object_t<C>(sc, o, r, inv, &t, &prim) && !(t + ERR_MARGIN >= dist)) return false;
+            if (object_t<C>(sc, o, r, inv, &t, &prim, dist) && !(t + ERR_MARGIN >= dist)) return false;
         }
     }
     return true;

@@ -166,6 +166,18 @@ hipError_t launch_finalize_f64(const RenderArgs& a, const double* sub_buf, hipSt
     return hipGetLastError();
 }
 
+// Diagnostic builds: read and clear the traversal counters (all zeros otherwise).
+extern "C" int rt_debug_counters(unsigned long long out[8]) {
+#if RT_DEBUG_COUNTERS
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(g_dbg)) != hipSuccess) return -1;
+    unsigned long long z[8] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), z, sizeof(z)) != hipSuccess) return -1;
+#else
+    for (int i = 0; i < 8; ++i) out[i] = 0;
+#endif
+    return 0;
+}
+
 hipError_t launch_trace_f64(const DevScene& sc, long n, const double* o, const double* d, double* t, int32_t* obj,
                             double* pos, double* nrm, hipStream_t st) {
     if (n <= 0) return hipSuccess;
