@@ -65,12 +65,20 @@ RT_DEV void begin_sample(const DevScene& sc, const RenderArgs& a, const SubPixel
     ps.kind = K_CAMERA;
 }
 
+// A shadow ray whose mesh test is deferred to the wavefront's k_wf_shadow_mesh (the analytic
+// objects already let it through). `c` is the NEE term already weighted by the path throughput.
+struct ShadowDefer {
+    bool pending;
+    V3 o, d, c;
+    double dist;
+};
+
 // Shades the hit `hr` of ps.ray. Returns true when the path continues (ps.ray is the next ray to
 // trace), false when this sample's radiance ps.L is final. The shadow ray of next-event estimation
 // is traced inline.
 template <class C>
 RT_DEV bool shade_vertex(const DevScene& sc, LdsTab* tab, const RenderArgs& a, const SubPixel& sp, int smp, PathState& ps,
-                         const HitRec& hr) {
+                         const HitRec& hr, ShadowDefer* defer = nullptr) {
     if (hr.obj < 0) return false;  // no hit: R = 0 (scene.rs:157, :175, :233)
     const DevObject& obj = sc.objects[hr.obj];
     V3 x, nrm;
@@ -114,7 +122,27 @@ RT_DEV bool shade_vertex(const DevScene& sc, LdsTab* tab, const RenderArgs& a, c
     double r_sqr = dot(y - x, y - x);
     V3 lef = mult(ld3(sc.objects[sc.light].emitted), brdf_eval<C>(obj, nrm, ps.o, i));
     if (!is_zero(lef)) {  // a zero Le*f makes the term exactly 0: skip the shadow ray
-        double vis = visible<C>(sc, tab, x, y) ? 1. : 0.;
+        double vis;
+        if constexpr (C::mesh && C::compact) {
+            if (defer) {
+                // mutually_visible (scene.rs:258-270) split: analytic objects now, meshes deferred
+                V3 diff = y - x;
+                double dist = mag(diff);
+                Ray sr{x, diff / dist};
+                const RayInv inv = make_inv(sr.d);
+                vis = visible_analytic<C>(sc, tab, sr, inv, dist) ? 1. : 0.;
+                if (vis > 0. && mesh_candidate<C>(sc, sr, inv, dist)) {
+                    defer->pending = true;
+                    defer->o = sr.o;
+                    defer->d = sr.d;
+                    defer->dist = dist;
+                }
+            } else {
+                vis = visible<C>(sc, tab, x, y) ? 1. : 0.;
+            }
+        } else {
+            vis = visible<C>(sc, tab, x, y) ? 1. : 0.;
+        }
         V3 c;
         if (!use_mis) {
             c = lef * vis * dot(nrm, i) * dot(ny, -i) / (r_sqr * pdfA);
@@ -125,7 +153,8 @@ RT_DEV bool shade_vertex(const DevScene& sc, LdsTab* tab, const RenderArgs& a, c
             c = v3(0, 0, 0);
             if (vis > 0. && cosl > 0. && pdf_b > 0.) c = lef * dot(nrm, i) * ((pdf_l / (pdf_l + pdf_b)) / pdf_l);
         }
-        ps.L = ps.L + mult(ps.beta, c);
+        if (defer && defer->pending) defer->c = mult(ps.beta, c);  // added later iff no mesh occludes
+        else ps.L = ps.L + mult(ps.beta, c);
     }
     // Russian roulette + BSDF continuation (scene.rs:231-240)
     if (!(rng.uniform() < p)) return false;

@@ -668,6 +668,90 @@ RT_DEV bool visible(const DevScene& sc, LdsTab* tab, V3 x, V3 y) {
     return true;
 }
 
+// ---- pieces of trace_ray / mutually_visible for the wavefront's deferred mesh queries ----
+// (compact scenes only: analytic objects = axis planes, spheres, and non-mesh generic objects)
+template <class C>
+RT_DEV HitRec trace_analytic(const DevScene& sc, LdsTab* tab, const Ray& ray, const RayInv& inv) {
+    HitRec h{0.0, -1, -1};
+    auto visit = [&](double t, int idx, int prim) { consider(h, t, idx, prim); };
+    axis_planes<0>(sc, tab, ray, inv, visit);
+    axis_planes<1>(sc, tab, ray, inv, visit);
+    axis_planes<2>(sc, tab, ray, inv, visit);
+#pragma unroll
+    for (int i = 0; i < kMaxSpheres; ++i) {
+        double t;
+        if (i < sc.n_sph && sphere_c(RT_TAB_SPH(i), ray, &t)) consider(h, t, sc.sph_idx[i], -1);
+    }
+    for (int i = 0; i < sc.n_gen; ++i) {
+        const int idx = sc.gen_idx[i];
+        const DevObject& o = sc.objects[idx];
+        double t;
+        int prim = -1;
+        if (o.geom != GEOM_MESH && object_t<C>(sc, o, ray, inv, &t, &prim)) consider(h, t, idx, prim);
+    }
+    return h;
+}
+// Adds the meshes' hits to an analytic closest hit (Scene::trace_ray's loop over the mesh objects).
+template <class C>
+RT_DEV void trace_meshes(const DevScene& sc, const Ray& ray, const RayInv& inv, HitRec& h) {
+    for (int i = 0; i < sc.n_gen; ++i) {
+        const int idx = sc.gen_idx[i];
+        const DevObject& o = sc.objects[idx];
+        if (o.geom != GEOM_MESH) continue;
+        double t;
+        int prim = -1;
+        if (mesh_hit(sc, sc.meshes[o.mesh], ray, inv, h.obj >= 0 ? h.t : INFINITY, &t, &prim)) consider(h, t, idx, prim);
+    }
+}
+// Could any mesh change this ray's result (closest hit so far at tmax / shadow distance tmax)?
+template <class C>
+RT_DEV bool mesh_candidate(const DevScene& sc, const Ray& ray, const RayInv& inv, double tmax) {
+    bool any = false;
+    for (int i = 0; i < sc.n_gen; ++i) {
+        const DevObject& o = sc.objects[sc.gen_idx[i]];
+        if (o.geom == GEOM_MESH && sc.meshes[o.mesh].n_nodes > 0) {
+            const DevMesh& m = sc.meshes[o.mesh];
+            any |= near_box(m.root_box, ray, inv, m.cull_pad, tmax);
+        }
+    }
+    return any;
+}
+// mutually_visible split: the analytic objects here, the meshes later (mesh_occludes).
+template <class C>
+RT_DEV bool visible_analytic(const DevScene& sc, LdsTab* tab, const Ray& r, const RayInv& inv, double dist) {
+    const double ERR_MARGIN = 0.001;
+    bool occluded = false;
+    auto visit = [&](double t, int, int) { occluded |= !(t + ERR_MARGIN >= dist); };
+    axis_planes<0>(sc, tab, r, inv, visit);
+    axis_planes<1>(sc, tab, r, inv, visit);
+    axis_planes<2>(sc, tab, r, inv, visit);
+#pragma unroll
+    for (int i = 0; i < kMaxSpheres; ++i) {
+        double t;
+        if (i < sc.n_sph && sphere_c(RT_TAB_SPH(i), r, &t)) occluded |= !(t + ERR_MARGIN >= dist);
+    }
+    if (occluded) return false;
+    for (int i = 0; i < sc.n_gen; ++i) {
+        const DevObject& o = sc.objects[sc.gen_idx[i]];
+        double t;
+        int prim;
+        if (o.geom != GEOM_MESH && object_t<C>(sc, o, r, inv, &t, &prim, dist) && !(t + ERR_MARGIN >= dist)) return false;
+    }
+    return true;
+}
+template <class C>
+RT_DEV bool mesh_occludes(const DevScene& sc, const Ray& r, const RayInv& inv, double dist) {
+    const double ERR_MARGIN = 0.001;
+    for (int i = 0; i < sc.n_gen; ++i) {
+        const DevObject& o = sc.objects[sc.gen_idx[i]];
+        if (o.geom != GEOM_MESH) continue;
+        double t;
+        int prim;
+        if (mesh_hit(sc, sc.meshes[o.mesh], r, inv, dist, &t, &prim) && !(t + ERR_MARGIN >= dist)) return true;
+    }
+    return false;
+}
+
 // ---------------------------------------------------------------- BRDF (scene.rs:30-123)
 template <class C>
 RT_DEV V3 brdf_eval(const DevObject& o, V3 n, V3 out, V3 in) {

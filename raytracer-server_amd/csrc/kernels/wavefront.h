@@ -40,7 +40,12 @@ struct Workspace {
     double* hit_t = nullptr;
     int32_t* hit_obj = nullptr;
     int32_t* hit_prim = nullptr;
-    uint32_t* ctrl = nullptr;  // [0],[1] stream counts, [2] next subpixel, [3] spare
+    uint32_t* ctrl = nullptr;  // [0],[1] stream counts, [2] next subpixel, [3] spare, [4] |Q1|, [5] |Q2|
+    // deferred mesh queries (scenes with meshes): Q1 = paths whose extension ray may hit a mesh,
+    // Q2 = shadow rays the analytic objects let through that a mesh may still block
+    int32_t* q1 = nullptr;
+    int32_t* q2_pos = nullptr;   // the path's index in the output stream
+    double* q2 = nullptr;        // [10][slots]: origin xyz, dir xyz, dist, weighted NEE term xyz
     double* sub_buf = nullptr; // subpixel means when the caller passes none
     size_t sub_cap = 0;
     uint32_t* host_ctrl = nullptr;  // pinned mirror of ctrl

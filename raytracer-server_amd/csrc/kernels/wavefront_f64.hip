@@ -8,6 +8,12 @@
 //                 by a fresh subpixel from a global work counter (regeneration). Survivors and
 //                 regenerated paths are compacted into stream B: wave ballot -> popcount prefix ->
 //                 one atomicAdd per wave, every lane writing its state at base + prefix.
+// Scenes with meshes: extend traces the analytic objects and queues (Q1) the rays a mesh could
+// still change; k_wf_mesh_closest traverses exactly those, in full waves, and merges with the
+// reference's tie rule. Shade tests shadow rays against the analytic objects and queues (Q2) the
+// ones a mesh could still block; k_wf_shadow_mesh adds their NEE term to the path if unblocked.
+// Paths that end with a pending shadow stay in the stream one more bounce as K_DONE, so every
+// path's radiance is summed in exactly the megakernel's order (bit-identical images).
 // Streams never hold two live paths of one subpixel, so each subpixel's mean is a sequential sum
 // in sample order (identical to server.rs:338-358) with no atomics on the accumulator.
 // k_wf_finalize turns the 4 subpixel means of each pixel into RGB8 (server.rs:360-368).
@@ -26,6 +32,7 @@ using namespace f64;
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int K_DONE = 3;  // path finished; waiting for a deferred shadow result
 
 RT_DEV void store_state(const PathStream& S, long i, const PathState& ps, int sub, int smp, bool mis) {
     S.ox[i] = ps.ray.o.x; S.oy[i] = ps.ray.o.y; S.oz[i] = ps.ray.o.z;
@@ -94,24 +101,93 @@ __global__ __launch_bounds__(kBlock) void k_wf_init(DevScene sc, RenderArgs a, P
         ctrl[0] = (uint32_t)n0;
         ctrl[1] = 0;
         ctrl[2] = (uint32_t)n0;  // next subpixel to hand out
+        ctrl[4] = 0;
+        ctrl[5] = 0;
     }
 }
 
 template <int F>
 __global__ __launch_bounds__(kBlock) void k_wf_extend(DevScene sc, PathStream A, const uint32_t* cnt_in,
                                                        uint32_t* cnt_out, double* __restrict__ ht,
-                                                       int32_t* __restrict__ hobj, int32_t* __restrict__ hprim) {
+                                                       int32_t* __restrict__ hobj, int32_t* __restrict__ hprim,
+                                                       int32_t* __restrict__ q1, uint32_t* q1_cnt, uint32_t* q2_cnt) {
+    using C = Cfg<F>;
+    constexpr bool kDefer = C::mesh && C::compact;
     __shared__ double s_tab[kTabSize];
-    LdsTab* tab = stage_tables<Cfg<F>>(sc, s_tab);
+    LdsTab* tab = stage_tables<C>(sc, s_tab);
     const long n = (long)*cnt_in;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_out = 0;  // stream B is refilled by k_wf_shade
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *cnt_out = 0;  // stream B is refilled by k_wf_shade
+        *q2_cnt = 0;   // Q2 is refilled by k_wf_shade (the previous k_wf_shadow_mesh has drained it)
+    }
     const long stride = (long)gridDim.x * blockDim.x;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    for (long base = (long)blockIdx.x * blockDim.x; base < n; base += stride) {
+        const long i = base + threadIdx.x;
+        bool cand = false;
+        if (i < n) {
+            Ray r{v3(A.ox[i], A.oy[i], A.oz[i]), v3(A.dx[i], A.dy[i], A.dz[i])};
+            if ((A.dk[i] & 3) == K_DONE) {
+                hobj[i] = -2;
+            } else if constexpr (kDefer) {
+                const RayInv inv = make_inv(r.d);
+                HitRec h = trace_analytic<C>(sc, tab, r, inv);
+                ht[i] = h.t;
+                hobj[i] = h.obj;
+                hprim[i] = h.prim;
+                cand = mesh_candidate<C>(sc, r, inv, h.obj >= 0 ? h.t : INFINITY);
+            } else {
+                HitRec h = trace_closest<C>(sc, tab, r);
+                ht[i] = h.t;
+                hobj[i] = h.obj;
+                hprim[i] = h.prim;
+            }
+        }
+        if constexpr (kDefer) {
+            long pos = wave_append(q1_cnt, cand);
+            if (cand) q1[pos] = (int32_t)i;
+        }
+    }
+}
+
+// Mesh part of trace_ray for the queued rays: full waves of traversal work.
+template <int F>
+__global__ __launch_bounds__(kBlock) void k_wf_mesh_closest(DevScene sc, PathStream A, const int32_t* __restrict__ q1,
+                                                            const uint32_t* q1_cnt, double* __restrict__ ht,
+                                                            int32_t* __restrict__ hobj, int32_t* __restrict__ hprim) {
+    using C = Cfg<F>;
+    const long n = (long)*q1_cnt;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
+        const long i = q1[q];
         Ray r{v3(A.ox[i], A.oy[i], A.oz[i]), v3(A.dx[i], A.dy[i], A.dz[i])};
-        HitRec h = trace_closest<Cfg<F>>(sc, tab, r);
+        const RayInv inv = make_inv(r.d);
+        HitRec h{ht[i], hobj[i], hprim[i]};
+        trace_meshes<C>(sc, r, inv, h);
         ht[i] = h.t;
         hobj[i] = h.obj;
         hprim[i] = h.prim;
+    }
+}
+
+// Mesh part of mutually_visible for the queued shadow rays; unblocked ones add their NEE term.
+template <int F>
+__global__ __launch_bounds__(kBlock) void k_wf_shadow_mesh(DevScene sc, PathStream B, const int32_t* __restrict__ q2_pos,
+                                                           const double* __restrict__ q2, const uint32_t* q2_cnt,
+                                                           long slots, uint32_t* q1_cnt) {
+    using C = Cfg<F>;
+    const long n = (long)*q2_cnt;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *q1_cnt = 0;  // Q1 is refilled by the next k_wf_extend
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
+        Ray r{v3(q2[q], q2[slots + q], q2[2 * slots + q]), v3(q2[3 * slots + q], q2[4 * slots + q], q2[5 * slots + q])};
+        const double dist = q2[6 * slots + q];
+        const RayInv inv = make_inv(r.d);
+        if (!mesh_occludes<C>(sc, r, inv, dist)) {
+            const long p = q2_pos[q];
+            B.lx[p] = B.lx[p] + q2[7 * slots + q];
+            B.ly[p] = B.ly[p] + q2[8 * slots + q];
+            B.lz[p] = B.lz[p] + q2[9 * slots + q];
+        }
     }
 }
 
@@ -121,9 +197,12 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, 
                                                       long nsub, const double* __restrict__ ht,
                                                       const int32_t* __restrict__ hobj,
                                                       const int32_t* __restrict__ hprim, double* sub_buf,
-                                                      unsigned long long* counters) {
+                                                      unsigned long long* counters, int32_t* __restrict__ q2_pos,
+                                                      double* __restrict__ q2, uint32_t* q2_cnt, long slots) {
+    using C = Cfg<F>;
+    constexpr bool kDefer = C::mesh && C::compact;
     __shared__ double s_tab[kTabSize];
-    LdsTab* tab = stage_tables<Cfg<F>>(sc, s_tab);
+    LdsTab* tab = stage_tables<C>(sc, s_tab);
     const long n = (long)*cnt_in;
     const long stride = (long)gridDim.x * blockDim.x;
     const bool mis = a.mis != 0;
@@ -133,15 +212,28 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, 
         const long i = base + threadIdx.x;
         const bool active = i < n;
         PathState ps;
+        ShadowDefer sd;
+        sd.pending = false;
         int sub = 0, smp = 0;
         bool emit = false;
         if (active) {
             load_state(A, i, ps, &sub, &smp, mis);
-            HitRec hr{ht[i], hobj[i], hprim[i]};
-            nverts += hr.obj >= 0;
             SubPixel sp = subpixel_of(a, sub);
-            emit = shade_vertex<Cfg<F>>(sc, tab, a, sp, smp, ps, hr);
-            if (!emit) {
+            bool finished;
+            if (ps.kind == K_DONE) {
+                finished = true;  // its deferred shadow has been resolved: fold it in now
+            } else {
+                HitRec hr{ht[i], hobj[i], hprim[i]};
+                nverts += hr.obj >= 0;
+                emit = shade_vertex<C>(sc, tab, a, sp, smp, ps, hr, kDefer ? &sd : nullptr);
+                finished = !emit;
+                if (finished && sd.pending) {
+                    ps.kind = K_DONE;  // keep the path one more bounce for its shadow result
+                    emit = true;
+                    finished = false;
+                }
+            }
+            if (finished) {
                 // sample finished: sequential mean update (server.rs:357-358), then regenerate
                 double* acc = sub_buf + (size_t)sub * 3;
                 acc[0] = acc[0] + ps.L.x * a.inv_n;
@@ -165,6 +257,22 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, 
         }
         long pos = wave_append(cnt_out, emit);
         if (emit) store_state(B, pos, ps, sub, smp, mis);
+        if constexpr (kDefer) {
+            long qp = wave_append(q2_cnt, sd.pending);
+            if (sd.pending) {
+                q2_pos[qp] = (int32_t)pos;
+                q2[qp] = sd.o.x;
+                q2[slots + qp] = sd.o.y;
+                q2[2 * slots + qp] = sd.o.z;
+                q2[3 * slots + qp] = sd.d.x;
+                q2[4 * slots + qp] = sd.d.y;
+                q2[5 * slots + qp] = sd.d.z;
+                q2[6 * slots + qp] = sd.dist;
+                q2[7 * slots + qp] = sd.c.x;
+                q2[8 * slots + qp] = sd.c.y;
+                q2[9 * slots + qp] = sd.c.z;
+            }
+        }
     }
     if (counters) {
         unsigned long long v = nverts;
@@ -177,10 +285,18 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, 
 template <int F>
 void launch_bounce_t(dim3 g, hipStream_t st, const DevScene& sc, const RenderArgs& a, Workspace& ws, int cur, int nxt,
                      long nsub, double* sub_buf, unsigned long long* counters) {
+    constexpr bool kDefer = Cfg<F>::mesh && Cfg<F>::compact;
     hipLaunchKernelGGL(k_wf_extend<F>, g, dim3(kBlock), 0, st, sc, ws.s[cur], ws.ctrl + cur, ws.ctrl + nxt, ws.hit_t,
-                       ws.hit_obj, ws.hit_prim);
+                       ws.hit_obj, ws.hit_prim, ws.q1, ws.ctrl + 4, ws.ctrl + 5);
+    if (kDefer)
+        hipLaunchKernelGGL(k_wf_mesh_closest<F>, g, dim3(kBlock), 0, st, sc, ws.s[cur], (const int32_t*)ws.q1,
+                           (const uint32_t*)(ws.ctrl + 4), ws.hit_t, ws.hit_obj, ws.hit_prim);
     hipLaunchKernelGGL(k_wf_shade<F>, g, dim3(kBlock), 0, st, sc, a, ws.s[cur], ws.s[nxt], ws.ctrl + cur,
-                       ws.ctrl + nxt, ws.ctrl + 2, nsub, ws.hit_t, ws.hit_obj, ws.hit_prim, sub_buf, counters);
+                       ws.ctrl + nxt, ws.ctrl + 2, nsub, ws.hit_t, ws.hit_obj, ws.hit_prim, sub_buf, counters,
+                       ws.q2_pos, ws.q2, ws.ctrl + 5, (long)ws.slots);
+    if (kDefer)
+        hipLaunchKernelGGL(k_wf_shadow_mesh<F>, g, dim3(kBlock), 0, st, sc, ws.s[nxt], (const int32_t*)ws.q2_pos,
+                           (const double*)ws.q2, (const uint32_t*)(ws.ctrl + 5), (long)ws.slots, ws.ctrl + 4);
 }
 
 void launch_bounce(int features, dim3 g, hipStream_t st, const DevScene& sc, const RenderArgs& a, Workspace& ws,
@@ -238,8 +354,9 @@ hipError_t Workspace::ensure_slots(size_t n) {
     // per stream: 19 f64 arrays + 2 u64 + 3 i32 arrays; hit: f64 + 2 i32
     const size_t per_stream = n * (21 * sizeof(double) + 3 * sizeof(int32_t));
     const size_t hits = n * (sizeof(double) + 2 * sizeof(int32_t));
+    const size_t queues = n * (2 * sizeof(int32_t) + 10 * sizeof(double));
     const size_t pad = 64 * 1024;
-    e = hipMalloc(&blob, 2 * per_stream + hits + pad);
+    e = hipMalloc(&blob, 2 * per_stream + hits + queues + pad);
     if (e != hipSuccess) { blob = nullptr; return e; }
     char* p = (char*)blob;
     auto take = [&](size_t bytes) {
@@ -261,6 +378,9 @@ hipError_t Workspace::ensure_slots(size_t n) {
     hit_t = (double*)take(n * sizeof(double));
     hit_obj = (int32_t*)take(n * sizeof(int32_t));
     hit_prim = (int32_t*)take(n * sizeof(int32_t));
+    q1 = (int32_t*)take(n * sizeof(int32_t));
+    q2_pos = (int32_t*)take(n * sizeof(int32_t));
+    q2 = (double*)take(10 * n * sizeof(double));
     slots = n;
     return hipSuccess;
 }
