@@ -277,29 +277,7 @@ RT_DEV bool near_box(const double* bx, const Ray& r, const RayInv& inv, double p
     return t0 <= t1 && t0 <= tmax * (1.0 + 1e-9) + 1e-9;
 }
 
-// Diagnostic build only (make EXTRA=-DRT_DEBUG_COUNTERS=1): traversal work counters.
-#if RT_DEBUG_COUNTERS
-__device__ unsigned long long g_dbg[8];  // 0 mesh calls, 1 past cull, 2 node visits, 3 box tests, 4 tri tests
-#define RT_DBG(i) atomicAdd(&g_dbg[i], 1ull)
-#else
-#define RT_DBG(i) ((void)0)
-#endif
-
-// Leaf: nearest triangle, strict < (geometry.rs:1276-1293).
-RT_DEV bool leaf_hit(const DevScene& sc, int off, int cnt, const Ray& ray, double* t, int* prim) {
-    bool any = false;
-    for (int r = 0; r < cnt; ++r) {
-        int ti = sc.tri_ref[off + r];
-        double tt;
-        RT_DBG(4);
-        if (tri_t(sc.tris[ti], ray, &tt)) {
-            if (!any || tt < *t) { *t = tt; *prim = ti; any = true; }
-        }
-    }
-    return any;
-}
-
-// shared by both traversals
+// shared by the traversal's child-order sort
 RT_DEV bool sqrt_gt(double a2, double b2) {
     // sqrt(a2) > sqrt(b2) after rounding, without the square roots unless the radicands are within
     // a few ulps (sqrt is monotone; a relative gap > 2^-50 survives both roundings).
@@ -307,27 +285,133 @@ RT_DEV bool sqrt_gt(double a2, double b2) {
     if (a2 > b2 * (1.0 + 0x1p-50)) return true;
     return sqrt(a2) > sqrt(b2);
 }
-#if !RT_TRAVERSAL_FLAT
-// Octree::intersect (geometry.rs:1237-1295), stackless (default traversal): the per-ray child order (root-octant
-// centre distances, insertion-sorted, strict >) is identical at every level, so the DFS resumes
-// from parent links + the child's slot rank instead of a stack. Same visiting order and the same
-// first-leaf-with-a-hit exit as the reference recursion; no per-lane stack memory.
-RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax, double* t,
-                     int* prim) {
+
+// BoundingBox::intersect(..).is_some() (geometry.rs:977-1036) for all 8 octants of the box
+// [mn, mx] at once; bit i = octant i (bit2 = x, bit1 = y, bit0 = z upper half, geometry.rs:1067-1099).
+// An octant's six faces lie on 9 planes (min / centre / max per axis), so each plane's crossing
+// (t, and the point's two other coordinates) is computed once and shared by the 4 octants whose
+// faces lie on it. Every quantity is the one box_hit computes for that octant's box (same
+// division, same eval, same bounds: the octant boxes are built from exactly this centre), and
+// box_hit's result is the OR over faces, so the mask equals eight box_hit calls bit for bit.
+RT_DEV uint32_t octant_mask(const double* mn, const double* mx, const Ray& r, const RayInv& inv) {
+    const double EPS = 0.0000001;
+    const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+    double c[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) c[k] = (mn[k] + mx[k]) / 2.0;  // BoundingBox::center
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {  // planes normal to axis k
+        const int u = k == 0 ? 1 : 0, v = k == 2 ? 1 : 2;  // the other two axes, u < v
+        // octant index bit of axis a: 4 >> a
+        const uint32_t bk = 4u >> k, bu = 4u >> u, bv = 4u >> v;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const double X = j == 0 ? mn[k] : j == 1 ? c[k] : mx[k];
+            const double num = X - o[k];
+            const double t = k == 0 ? div_x(num, r, inv) : k == 1 ? div_y(num, r, inv) : div_z(num, r, inv);
+            if (t >= EPS) {
+                const double pu = o[u] + t * d[u], pv = o[v] + t * d[v];  // Ray::eval
+                const bool ul = mn[u] <= pu && pu <= c[u], uh = c[u] <= pu && pu <= mx[u];
+                const bool vl = mn[v] <= pv && pv <= c[v], vh = c[v] <= pv && pv <= mx[v];
+                // octants with this face, for the lower (j <= 1) and upper (j >= 1) half along k
+                uint32_t q = 0;
+                q |= (ul && vl) ? (1u << 0) : 0u;
+                q |= (ul && vh) ? (1u << bv) : 0u;
+                q |= (uh && vl) ? (1u << bu) : 0u;
+                q |= (uh && vh) ? (1u << (bu + bv)) : 0u;
+                if (j <= 1) m |= q;
+                if (j >= 1) m |= q << bk;
+            }
+        }
+    }
+    return m;
+}
+
+// Diagnostic build only (make EXTRA=-DRT_DEBUG_COUNTERS=1): traversal work counters.
+#if RT_DEBUG_COUNTERS
+__device__ unsigned long long g_dbg[8];  // 0 walks, 1 past cull, 2 node visits, 3 leaves, 4 tri tests, 5 steps
+#define RT_DBG(i) atomicAdd(&g_dbg[i], 1ull)
+#else
+#define RT_DBG(i) ((void)0)
+#endif
+
+// Octree::intersect (geometry.rs:1237-1295) as a resumable per-lane walk.
+// The reference visits a node's children in one order per ray (distances from the ray origin to
+// the ROOT box's octant centres, insertion-sorted with strict >, geometry.rs:1248-1260), descends
+// into the first child whose box the ray hits, and returns the first subtree with any hit (a leaf:
+// its nearest triangle, strict <, geometry.rs:1276-1293). The order is the same at every level, so
+// the walk keeps, per level, the 8-bit mask of the children still to visit (in visiting order)
+// instead of a stack of nodes, resumes at the parent through node_up, and rebuilds boxes from the
+// root along the path of octant slots. Same visits, same early exit, same result bits.
+// Each walk_step does one unit of work (a triangle test, a backtrack, or a child pick that either
+// opens a leaf or descends and masks the new node's children), so a wave can interleave walks of
+// different lengths and refill lanes whose walk ended (persistent traversal kernels).
+struct OctWalk {
+    double mn[3], mx[3];  // box of `cur`
+    int32_t kid[8];       // child table of `cur`
+    int32_t cur, depth;
+    uint32_t path;        // octant slot taken at each level, 3 bits per level (max depth 10)
+    uint32_t pm;          // children of `cur` still to visit, bit q = visiting rank q
+    uint64_t stk;         // pm of the ancestors at levels 0..7, 8 bits each
+    uint32_t stk8;        // level 8 (parents exist at depths 0..9; MAX_DEPTH = 10)
+    uint32_t order, rank; // nibble q = octant visited q-th; nibble i = rank of octant i
+    int32_t lpos, lend;   // leaf triangle cursor
+    int32_t best;         // nearest triangle so far in the current leaf (ltri index), -1 none
+    double bt;
+};
+
+RT_DEV void walk_load_kids(const DevScene& sc, OctWalk& w) {
+    const int4* k4 = reinterpret_cast<const int4*>(sc.node_kids + 8 * (size_t)w.cur);
+    const int4 a = k4[0], b = k4[1];
+    w.kid[0] = a.x; w.kid[1] = a.y; w.kid[2] = a.z; w.kid[3] = a.w;
+    w.kid[4] = b.x; w.kid[5] = b.y; w.kid[6] = b.z; w.kid[7] = b.w;
+}
+// Mask `cur`'s existing children whose boxes the ray hits, permuted to visiting order.
+RT_DEV void walk_enter(const DevScene& sc, const Ray& ray, const RayInv& inv, OctWalk& w) {
+    RT_DBG(2);
+    walk_load_kids(sc, w);
+    uint32_t m = octant_mask(w.mn, w.mx, ray, inv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m &= w.kid[i] == kKidEmpty ? ~(1u << i) : ~0u;
+    uint32_t pm = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) pm |= ((m >> ((w.order >> (4 * q)) & 0xF)) & 1u) << q;
+    w.pm = pm;
+}
+
+// Starts a walk; false if the ray cannot produce a usable hit on this mesh (empty mesh, or the
+// conservative near_box cull). tmax: see near_box.
+RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax,
+                       OctWalk& w) {
     if (m.n_nodes == 0) return false;
     RT_DBG(0);
     if (!near_box(m.root_box, ray, inv, m.cull_pad, tmax)) return false;
     RT_DBG(1);
-    const int root = m.node_base;
-    NodeMeta rm = sc.node_meta[root];
-    if (rm.leaf_off >= 0) return leaf_hit(sc, rm.leaf_off, rm.leaf_cnt, ray, t, prim);
+    w.best = -1;
+    w.bt = 0.0;
+    w.cur = m.node_base;
+    w.depth = 0;
+    w.path = 0;
+    w.stk = 0;
+    w.stk8 = 0;
+    w.pm = 0;
+    if (m.root_leaf >= 0) {
+        const int2 ls = sc.leaf_span[m.root_leaf];
+        w.lpos = ls.x;
+        w.lend = ls.x + ls.y;
+        w.order = 0x76543210u;
+        w.rank = 0x76543210u;
+        return true;
+    }
+    w.lpos = w.lend = 0;
     double d2[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         V3 dv = ld3(m.oct_center[i]) - ray.o;
         d2[i] = dv.x * dv.x + dv.y * dv.y + dv.z * dv.z;  // mag()'s radicand, same operation order
     }
-    uint32_t order = 0x76543210u;  // nibble k = octant visited k-th
+    uint32_t order = 0x76543210u;
 #pragma unroll
     for (int i = 1; i < 8; ++i) {
 #pragma unroll
@@ -342,141 +426,104 @@ RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const
             }
         }
     }
-    uint32_t rank = 0;  // nibble i = position of octant i in `order`
+    uint32_t rank = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) rank |= (uint32_t)k << (4 * ((order >> (4 * k)) & 0xF));
-
-    int cur = root;
-    int k = 0;
-    while (true) {
-        int found = -1;
-        RT_DBG(2);
-        const int* ch = sc.node_child + 8 * (size_t)cur;
-        for (; k < 8; ++k) {
-            int oi = (order >> (4 * k)) & 0xF;
-            int c = ch[oi];
-            if (c >= 0) RT_DBG(3);
-            if (c >= 0 && box_hit(sc.node_box + 6 * (size_t)c, ray, inv)) { found = c; break; }
-        }
-        if (found >= 0) {
-            NodeMeta fm = sc.node_meta[found];
-            if (fm.leaf_off >= 0) {
-                if (leaf_hit(sc, fm.leaf_off, fm.leaf_cnt, ray, t, prim)) return true;
-                ++k;  // next sibling
-            } else {
-                cur = found;
-                k = 0;
-            }
-            continue;
-        }
-        if (cur == root) return false;
-        NodeMeta cm = sc.node_meta[cur];
-        k = (int)((rank >> (4 * cm.slot)) & 0xF) + 1;
-        cur = cm.parent;
+    w.order = order;
+    w.rank = rank;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        w.mn[k] = m.root_box[k];
+        w.mx[k] = m.root_box[3 + k];
     }
+    walk_enter(sc, ray, inv, w);
+    return true;
 }
 
-#else
-// Octree::intersect (geometry.rs:1237-1295) as a flat per-lane state machine.
-// The reference visits children in an order fixed per ray (distances from the ray origin to the
-// ROOT box's octant centres, insertion-sorted with strict >, geometry.rs:1248-1260) and returns the
-// first subtree with any hit (leaf: nearest, strict <). The order is the same at every level, so
-// the DFS resumes from parent links + the child's rank instead of a stack. Each loop iteration does
-// exactly one box test or one triangle test per lane, so a divergent wave pays max(total steps)
-// rather than max(nodes) x max(children per node); empty octants are skipped with a permuted child
-// bitmask. Same visiting order, same early exit, same result bits.
+enum : int { WALK_RUN = 0, WALK_HIT = 1, WALK_MISS = 2 };
+
+// One unit of work. On WALK_HIT, *t / *prim hold the first hit subtree's nearest triangle.
+RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w, double* t,
+                     int* prim) {
+    RT_DBG(5);
+    if (w.lpos < w.lend) {  // one triangle of the open leaf
+        RT_DBG(4);
+        double tt;
+        if (tri_t(sc.ltris[w.lpos], ray, &tt) && (w.best < 0 || tt < w.bt)) {
+            w.bt = tt;
+            w.best = w.lpos;
+        }
+        if (++w.lpos < w.lend) return WALK_RUN;
+        if (w.best >= 0) {  // the first leaf with a hit wins (geometry.rs:1267-1269)
+            *t = w.bt;
+            *prim = sc.ltri_id[w.best];
+            return WALK_HIT;
+        }
+        return (w.depth == 0 && m.root_leaf >= 0) ? WALK_MISS : WALK_RUN;
+    }
+    if (w.pm == 0) {  // `cur` exhausted: resume at its parent
+        if (w.depth == 0) return WALK_MISS;
+        w.cur = sc.node_up[w.cur].x;
+        const int lv = --w.depth;
+        w.pm = lv < 8 ? (uint32_t)(w.stk >> (8 * lv)) & 0xFFu : w.stk8;
+        w.path &= (1u << (3 * lv)) - 1u;
+        walk_load_kids(sc, w);
+        // the parent's box, rebuilt from the root along the path (the build's own arithmetic)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            w.mn[k] = m.root_box[k];
+            w.mx[k] = m.root_box[3 + k];
+        }
+        for (int l = 0; l < lv; ++l) {
+            const uint32_t oi = (w.path >> (3 * l)) & 7u;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const double c = (w.mn[k] + w.mx[k]) / 2.0;
+                if ((oi >> (2 - k)) & 1u) w.mn[k] = c; else w.mx[k] = c;
+            }
+        }
+        return WALK_RUN;
+    }
+    const int q = __builtin_ctz(w.pm);
+    w.pm &= w.pm - 1u;
+    const uint32_t oi = (w.order >> (4 * q)) & 0xF;
+    int32_t c = w.kid[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) c = oi == (uint32_t)j ? w.kid[j] : c;
+    if (c <= -2) {  // open a leaf
+        RT_DBG(3);
+        const int2 ls = sc.leaf_span[-2 - c];
+        w.lpos = ls.x;
+        w.lend = ls.x + ls.y;
+        w.best = -1;
+        return WALK_RUN;
+    }
+    // descend: push the remaining mask of `cur`, take the octant's box
+    const int lv = w.depth;
+    if (lv < 8) w.stk = (w.stk & ~(0xFFull << (8 * lv))) | ((uint64_t)w.pm << (8 * lv));
+    else w.stk8 = w.pm;
+    w.path |= oi << (3 * lv);
+    w.depth = lv + 1;
+    w.cur = c;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double cc = (w.mn[k] + w.mx[k]) / 2.0;
+        if ((oi >> (2 - k)) & 1u) w.mn[k] = cc; else w.mx[k] = cc;
+    }
+    walk_enter(sc, ray, inv, w);
+    return WALK_RUN;
+}
+
+// Whole traversal in one call (megakernel / trace kernel).
 RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax, double* t,
                      int* prim) {
-    if (m.n_nodes == 0) return false;
-    if (!near_box(m.root_box, ray, inv, m.cull_pad, tmax)) return false;
-    const int root = m.node_base;
-    NodeMeta rm = sc.node_meta[root];
-    if (rm.leaf_off >= 0) return leaf_hit(sc, rm.leaf_off, rm.leaf_cnt, ray, t, prim);
-    // per-ray child order: insertion sort on (distance^2, octant) pairs held in registers
-    double d2[8];
-    int oc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        V3 dv = ld3(m.oct_center[i]) - ray.o;
-        d2[i] = dv.x * dv.x + dv.y * dv.y + dv.z * dv.z;  // mag()'s radicand, same operation order
-        oc[i] = i;
+    OctWalk w;
+    if (!walk_begin(sc, m, ray, inv, tmax, w)) return false;
+    int st;
+    while ((st = walk_step(sc, m, ray, inv, w, t, prim)) == WALK_RUN) {
     }
-#pragma unroll
-    for (int i = 1; i < 8; ++i) {
-#pragma unroll
-        for (int j = i; j > 0; --j) {
-            // a sorted prefix has no inversion, so comparing past the insertion point swaps nothing:
-            // identical to the reference's early-exit loop
-            bool sw = sqrt_gt(d2[j - 1], d2[j]);
-            double td = d2[j - 1];
-            int to = oc[j - 1];
-            d2[j - 1] = sw ? d2[j] : td;
-            d2[j] = sw ? td : d2[j];
-            oc[j - 1] = sw ? oc[j] : to;
-            oc[j] = sw ? to : oc[j];
-        }
-    }
-    uint32_t order = 0, rank = 0;  // nibble k = octant visited k-th; nibble i = rank of octant i
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        order |= (uint32_t)oc[k] << (4 * k);
-        rank |= (uint32_t)k << (4 * oc[k]);
-    }
-    int cur = root;        // current parent
-    uint32_t pm = 0;       // existing children of `cur`, permuted to visiting order
-    int k = 0;             // next rank to test at `cur`
-    int lpos = 0, lend = 0;  // leaf triangle cursor (lpos < lend: inside a leaf)
-    bool any = false, enter = true;
-    while (true) {
-        if (lpos < lend) {
-            // one triangle test
-            int ti = sc.tri_ref[lpos];
-            double tt;
-            if (tri_t(sc.tris[ti], ray, &tt)) {
-                if (!any || tt < *t) { *t = tt; *prim = ti; any = true; }
-            }
-            if (++lpos == lend) {
-                if (any) return true;  // first leaf with a hit wins (geometry.rs:1267-1269)
-                ++k;
-            }
-            continue;
-        }
-        if (enter) {  // build the permuted child mask of `cur`
-            const int* ch = sc.node_child + 8 * (size_t)cur;
-            pm = 0;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) pm |= (uint32_t)(ch[(order >> (4 * q)) & 0xF] >= 0) << q;
-            enter = false;
-        }
-        const uint32_t rest = k < 8 ? (pm >> k) : 0u;
-        if (rest == 0u) {  // `cur` exhausted: resume at the parent, after cur's rank
-            if (cur == root) return false;
-            NodeMeta cm = sc.node_meta[cur];
-            k = (int)((rank >> (4 * cm.slot)) & 0xF) + 1;
-            cur = cm.parent;
-            enter = true;
-            continue;
-        }
-        k += __builtin_ctz(rest);
-        const int c = sc.node_child[8 * (size_t)cur + ((order >> (4 * k)) & 0xF)];
-        if (box_hit(sc.node_box + 6 * (size_t)c, ray, inv)) {
-            NodeMeta fm = sc.node_meta[c];
-            if (fm.leaf_off >= 0) {
-                lpos = fm.leaf_off;
-                lend = fm.leaf_off + fm.leaf_cnt;
-                if (lend == lpos) ++k;  // (empty leaves do not exist; defensive)
-            } else {
-                cur = c;
-                k = 0;
-                enter = true;
-            }
-        } else {
-            ++k;
-        }
-    }
+    return st == WALK_HIT;
 }
-
-#endif  // RT_TRAVERSAL_FLAT
 
 // Kernel specialisation by scene features (chosen on the host per scene/flags): code paths a
 // scene cannot reach are not compiled into its kernels, which keeps register pressure down.

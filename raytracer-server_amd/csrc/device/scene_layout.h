@@ -7,6 +7,10 @@
 
 #include <stdint.h>
 
+#include <hip/hip_runtime.h>
+
+#define RT_LAYOUT_FN __host__ __device__ inline
+
 namespace rt {
 
 enum : int32_t { GEOM_SPHERE = 0, GEOM_PLANE = 1, GEOM_MESH = 2 };
@@ -29,10 +33,12 @@ struct alignas(16) DevObject {
 };
 
 // Octree of one mesh, flattened in the reference's DFS pre-order (geometry.rs:1164-1216) so node
-// i here is node i of the reference's Vec<Node>. Indices in node_child / tri_ref are GLOBAL
-// (mesh bases already added).
+// i here is node i of the reference's Vec<Node> (plus node_base). Node boxes are NOT stored: a
+// child's box is the octant of its parent's box (geometry.rs:1067-1099), recomputed in registers
+// with the build's own arithmetic, so the traversal reads only the child table (32 B per node).
+// All indices are GLOBAL (mesh bases already added).
 struct alignas(16) DevMesh {
-    int32_t node_base, n_nodes, ref_base, n_refs;
+    int32_t node_base, n_nodes, root_leaf, max_depth;  // root_leaf: leaf id when the root is a leaf, else -1
     int32_t tri_base, n_tris, pad0, pad1;
     double root_box[6];       // Octree.bounding_box (min xyz, max xyz)
     double oct_center[8][3];  // centres of the ROOT box's octants: traversal order key (geometry.rs:1249-1260)
@@ -41,11 +47,11 @@ struct alignas(16) DevMesh {
     double cull_pad;          // near_box padding: 1e-7 * max(1, |box coordinates|)
 };
 
-// Per node: x = leaf tri_ref offset (-1 for a parent), y = leaf count, z = parent node (-1 root),
-// w = octant slot in the parent.
-struct alignas(16) NodeMeta {
-    int32_t leaf_off, leaf_cnt, parent, slot;
-};
+// node_kids[node][8] entries: -1 empty octant, >= 0 parent node, <= -2 leaf id (-2 - entry).
+constexpr int32_t kKidEmpty = -1;
+RT_LAYOUT_FN int32_t kid_leaf(int32_t leaf) { return -2 - leaf; }
+// node_up[node] = {parent node (-1 at the root), octant slot in the parent}
+// leaf_span[leaf] = {first leaf triangle (index into ltris), count}
 
 // Triangle, precomputed exactly as Triangle::intersect derives it per call (geometry.rs:637-653):
 // a, ab = b - a, ac = c - a, n = ((c - a) x (b - a)).norm(). 12 doubles = 96 B.
@@ -65,11 +71,13 @@ constexpr int kTabSize = kTabSph + 4 * kMaxSpheres;  //   sphere (centre xyz, r^
 struct DevScene {
     const DevObject* objects;
     const DevMesh* meshes;
-    const NodeMeta* node_meta;
-    const int32_t* node_child;  // [node][8], -1 = empty octant
-    const double* node_box;     // [node][6]
-    const int32_t* tri_ref;     // leaf triangle lists
-    const DevTri* tris;
+    const int32_t* node_kids;   // [node][8], see kid_leaf
+    const int2* node_up;        // [node] {parent, slot}
+    const int2* leaf_span;      // [leaf] {first ltri, count}
+    const DevTri* ltris;        // leaf triangle lists as copies, in leaf order (the reference's leaves hold
+                                // (index, Triangle) copies too, geometry.rs:1131-1137)
+    const int32_t* ltri_id;     // [ltri] global triangle index (the hit's `prim`)
+    const DevTri* tris;         // per triangle (surface normal, mesh-light sampling)
     const double* tri_cum_area;  // per triangle, cumulative area within its mesh (mesh-light pick)
     int32_t n_objects, light, n_meshes, mesh_order_last;  // mesh_order_last: test meshes after analytic objects
     double cam_pos[3], cam_dir[3];

@@ -40,7 +40,7 @@ struct Workspace {
     double* hit_t = nullptr;
     int32_t* hit_obj = nullptr;
     int32_t* hit_prim = nullptr;
-    uint32_t* ctrl = nullptr;  // [0],[1] stream counts, [2] next subpixel, [3] spare, [4] |Q1|, [5] |Q2|
+    uint32_t* ctrl = nullptr;  // [0],[1] stream counts, [2] next subpixel, [3] spare, [4] |Q1|, [5] |Q2|, [6],[7] Q1/Q2 read heads
     // deferred mesh queries (scenes with meshes): Q1 = paths whose extension ray may hit a mesh,
     // Q2 = shadow rays the analytic objects let through that a mesh may still block
     int32_t* q1 = nullptr;

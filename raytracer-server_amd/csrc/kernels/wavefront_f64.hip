@@ -103,6 +103,8 @@ __global__ __launch_bounds__(kBlock) void k_wf_init(DevScene sc, RenderArgs a, P
         ctrl[2] = (uint32_t)n0;  // next subpixel to hand out
         ctrl[4] = 0;
         ctrl[5] = 0;
+        ctrl[6] = 0;
+        ctrl[7] = 0;
     }
 }
 
@@ -110,7 +112,8 @@ template <int F>
 __global__ __launch_bounds__(kBlock) void k_wf_extend(DevScene sc, PathStream A, const uint32_t* cnt_in,
                                                        uint32_t* cnt_out, double* __restrict__ ht,
                                                        int32_t* __restrict__ hobj, int32_t* __restrict__ hprim,
-                                                       int32_t* __restrict__ q1, uint32_t* q1_cnt, uint32_t* q2_cnt) {
+                                                       int32_t* __restrict__ q1, uint32_t* q1_cnt, uint32_t* q2_cnt,
+                                                       uint32_t* heads) {
     using C = Cfg<F>;
     constexpr bool kDefer = C::mesh && C::compact;
     __shared__ double s_tab[kTabSize];
@@ -119,6 +122,8 @@ __global__ __launch_bounds__(kBlock) void k_wf_extend(DevScene sc, PathStream A,
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         *cnt_out = 0;  // stream B is refilled by k_wf_shade
         *q2_cnt = 0;   // Q2 is refilled by k_wf_shade (the previous k_wf_shadow_mesh has drained it)
+        heads[0] = 0;  // Q1 / Q2 read heads of the persistent traversal kernels
+        heads[1] = 0;
     }
     const long stride = (long)gridDim.x * blockDim.x;
     for (long base = (long)blockIdx.x * blockDim.x; base < n; base += stride) {
@@ -149,46 +154,159 @@ __global__ __launch_bounds__(kBlock) void k_wf_extend(DevScene sc, PathStream A,
     }
 }
 
-// Mesh part of trace_ray for the queued rays: full waves of traversal work.
-template <int F>
-__global__ __launch_bounds__(kBlock) void k_wf_mesh_closest(DevScene sc, PathStream A, const int32_t* __restrict__ q1,
-                                                            const uint32_t* q1_cnt, double* __restrict__ ht,
-                                                            int32_t* __restrict__ hobj, int32_t* __restrict__ hprim) {
-    using C = Cfg<F>;
-    const long n = (long)*q1_cnt;
-    const long stride = (long)gridDim.x * blockDim.x;
-    for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
-        const long i = q1[q];
-        Ray r{v3(A.ox[i], A.oy[i], A.oz[i]), v3(A.dx[i], A.dy[i], A.dz[i])};
-        const RayInv inv = make_inv(r.d);
-        HitRec h{ht[i], hobj[i], hprim[i]};
-        trace_meshes<C>(sc, r, inv, h);
+// Persistent traversal of a query queue. Octree walks are long-tailed (a wave of independent rays
+// is busy as long as its longest walk: measured 4-6% lane utilisation with one query per lane), so
+// each lane runs a resumable walk (walk_step) and the wave refills lanes whose query finished from
+// the queue as soon as `refill` lanes are idle. One atomic per refill, per wave.
+// Query protocol (Q: query state type):
+//   start(qi, Q&) -> bool   load query qi; false if it needs no traversal (already finished)
+//   next_mesh(Q&) -> bool   begin the walk on the query's next candidate mesh; false when none left
+//   hit(Q&, t, prim) -> bool  a walk hit; true when the query is finished
+//   finish(Q&)              write the query's result
+template <class Q>
+RT_DEV void persistent_walks(const DevScene& sc, uint32_t n, uint32_t* head, int refill, Q& q) {
+    const int lane = (int)(threadIdx.x & 63);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    bool busy = false, drained = false;
+    while (true) {
+        const uint64_t idle = __ballot(!busy);
+        const int nidle = __popcll(idle);
+        if (!drained && (nidle >= refill || nidle == 64)) {
+            const int leader = __ffsll((unsigned long long)idle) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(head, (uint32_t)nidle);
+            base = __shfl(base, leader, 64);
+            if (base + (uint32_t)nidle >= n) drained = true;
+            if (!busy) {
+                const uint32_t qi = base + (uint32_t)__popcll(idle & lt);
+                if (qi < n && q.start(qi)) {
+                    busy = q.next_mesh();
+                    if (!busy) q.finish();
+                }
+            }
+        }
+        if (__ballot(busy) == 0) {
+            if (drained) break;
+            continue;
+        }
+        if (busy) {
+            double t;
+            int prim;
+            const int st = walk_step(sc, sc.meshes[q.mesh()], q.ray, q.inv, q.w, &t, &prim);
+            if (st != WALK_RUN) {
+                bool done = st == WALK_HIT && q.hit(t, prim);
+                if (!done) done = !q.next_mesh();
+                if (done) {
+                    q.finish();
+                    busy = false;
+                }
+            }
+        }
+    }
+}
+
+// Mesh part of trace_ray for the queued rays (Scene::trace_ray's loop over the mesh objects).
+struct ClosestQuery {
+    const DevScene& sc;
+    const PathStream& A;
+    const int32_t* q1;
+    double* ht;
+    int32_t* hobj;
+    int32_t* hprim;
+    long i;
+    Ray ray;
+    RayInv inv;
+    HitRec h;
+    int g;  // position in sc.gen_idx of the mesh being walked
+    OctWalk w;
+    RT_DEV bool start(uint32_t qi) {
+        i = q1[qi];
+        ray = Ray{v3(A.ox[i], A.oy[i], A.oz[i]), v3(A.dx[i], A.dy[i], A.dz[i])};
+        inv = make_inv(ray.d);
+        h = HitRec{ht[i], hobj[i], hprim[i]};
+        g = -1;
+        return true;
+    }
+    RT_DEV int mesh() const { return sc.objects[sc.gen_idx[g]].mesh; }
+    RT_DEV bool next_mesh() {
+        for (++g; g < sc.n_gen; ++g) {
+            const DevObject& o = sc.objects[sc.gen_idx[g]];
+            if (o.geom == GEOM_MESH && walk_begin(sc, sc.meshes[o.mesh], ray, inv, h.obj >= 0 ? h.t : INFINITY, w))
+                return true;
+        }
+        return false;
+    }
+    RT_DEV bool hit(double t, int prim) {
+        consider(h, t, sc.gen_idx[g], prim);
+        return false;
+    }
+    RT_DEV void finish() {
         ht[i] = h.t;
         hobj[i] = h.obj;
         hprim[i] = h.prim;
     }
+};
+
+template <int F>
+__global__ __launch_bounds__(kBlock) void k_wf_mesh_closest(DevScene sc, PathStream A, const int32_t* __restrict__ q1,
+                                                            const uint32_t* q1_cnt, uint32_t* q1_head,
+                                                            double* __restrict__ ht, int32_t* __restrict__ hobj,
+                                                            int32_t* __restrict__ hprim, int refill) {
+    ClosestQuery q{sc, A, q1, ht, hobj, hprim};
+    persistent_walks(sc, *q1_cnt, q1_head, refill, q);
 }
 
 // Mesh part of mutually_visible for the queued shadow rays; unblocked ones add their NEE term.
+struct ShadowQuery {
+    const DevScene& sc;
+    const PathStream& B;
+    const int32_t* q2_pos;
+    const double* q2;
+    long slots;
+    uint32_t qi;
+    Ray ray;
+    RayInv inv;
+    double dist;
+    bool occluded;
+    int g;
+    OctWalk w;
+    RT_DEV bool start(uint32_t q) {
+        qi = q;
+        ray = Ray{v3(q2[q], q2[slots + q], q2[2 * slots + q]), v3(q2[3 * slots + q], q2[4 * slots + q], q2[5 * slots + q])};
+        dist = q2[6 * slots + q];
+        inv = make_inv(ray.d);
+        occluded = false;
+        g = -1;
+        return true;
+    }
+    RT_DEV int mesh() const { return sc.objects[sc.gen_idx[g]].mesh; }
+    RT_DEV bool next_mesh() {
+        for (++g; g < sc.n_gen; ++g) {
+            const DevObject& o = sc.objects[sc.gen_idx[g]];
+            if (o.geom == GEOM_MESH && walk_begin(sc, sc.meshes[o.mesh], ray, inv, dist, w)) return true;
+        }
+        return false;
+    }
+    RT_DEV bool hit(double t, int) {
+        occluded = !(t + 0.001 >= dist);  // mesh_occludes / mutually_visible's ERR_MARGIN
+        return occluded;
+    }
+    RT_DEV void finish() {
+        if (occluded) return;
+        const long p = q2_pos[qi];
+        B.lx[p] = B.lx[p] + q2[7 * slots + qi];
+        B.ly[p] = B.ly[p] + q2[8 * slots + qi];
+        B.lz[p] = B.lz[p] + q2[9 * slots + qi];
+    }
+};
+
 template <int F>
 __global__ __launch_bounds__(kBlock) void k_wf_shadow_mesh(DevScene sc, PathStream B, const int32_t* __restrict__ q2_pos,
                                                            const double* __restrict__ q2, const uint32_t* q2_cnt,
-                                                           long slots, uint32_t* q1_cnt) {
-    using C = Cfg<F>;
-    const long n = (long)*q2_cnt;
+                                                           uint32_t* q2_head, long slots, uint32_t* q1_cnt, int refill) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *q1_cnt = 0;  // Q1 is refilled by the next k_wf_extend
-    const long stride = (long)gridDim.x * blockDim.x;
-    for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
-        Ray r{v3(q2[q], q2[slots + q], q2[2 * slots + q]), v3(q2[3 * slots + q], q2[4 * slots + q], q2[5 * slots + q])};
-        const double dist = q2[6 * slots + q];
-        const RayInv inv = make_inv(r.d);
-        if (!mesh_occludes<C>(sc, r, inv, dist)) {
-            const long p = q2_pos[q];
-            B.lx[p] = B.lx[p] + q2[7 * slots + q];
-            B.ly[p] = B.ly[p] + q2[8 * slots + q];
-            B.lz[p] = B.lz[p] + q2[9 * slots + q];
-        }
-    }
+    ShadowQuery q{sc, B, q2_pos, q2, slots};
+    persistent_walks(sc, *q2_cnt, q2_head, refill, q);
 }
 
 template <int F>
@@ -282,21 +400,43 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, 
     }
 }
 
+size_t env_size(const char* name, size_t dflt) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    long long x = std::atoll(v);
+    return x > 0 ? (size_t)x : dflt;
+}
+
+// Persistent traversal grid: as many blocks as are resident at once.
+template <class K>
+unsigned resident_grid(K kernel) {
+    int dev = 0, ncu = 256, nb = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kBlock, 0) != hipSuccess || nb < 1) nb = 1;
+    return (unsigned)(ncu * nb);
+}
+
 template <int F>
 void launch_bounce_t(dim3 g, hipStream_t st, const DevScene& sc, const RenderArgs& a, Workspace& ws, int cur, int nxt,
                      long nsub, double* sub_buf, unsigned long long* counters) {
     constexpr bool kDefer = Cfg<F>::mesh && Cfg<F>::compact;
+    static const unsigned g_closest = kDefer ? resident_grid(k_wf_mesh_closest<F>) : 1;
+    static const unsigned g_shadow = kDefer ? resident_grid(k_wf_shadow_mesh<F>) : 1;
+    static const int refill = (int)std::min<size_t>(64, std::max<size_t>(1, env_size("RT_WF_REFILL", 16)));
     hipLaunchKernelGGL(k_wf_extend<F>, g, dim3(kBlock), 0, st, sc, ws.s[cur], ws.ctrl + cur, ws.ctrl + nxt, ws.hit_t,
-                       ws.hit_obj, ws.hit_prim, ws.q1, ws.ctrl + 4, ws.ctrl + 5);
+                       ws.hit_obj, ws.hit_prim, ws.q1, ws.ctrl + 4, ws.ctrl + 5, ws.ctrl + 6);
     if (kDefer)
-        hipLaunchKernelGGL(k_wf_mesh_closest<F>, g, dim3(kBlock), 0, st, sc, ws.s[cur], (const int32_t*)ws.q1,
-                           (const uint32_t*)(ws.ctrl + 4), ws.hit_t, ws.hit_obj, ws.hit_prim);
+        hipLaunchKernelGGL(k_wf_mesh_closest<F>, dim3(g_closest), dim3(kBlock), 0, st, sc, ws.s[cur],
+                           (const int32_t*)ws.q1, (const uint32_t*)(ws.ctrl + 4), ws.ctrl + 6, ws.hit_t, ws.hit_obj,
+                           ws.hit_prim, refill);
     hipLaunchKernelGGL(k_wf_shade<F>, g, dim3(kBlock), 0, st, sc, a, ws.s[cur], ws.s[nxt], ws.ctrl + cur,
                        ws.ctrl + nxt, ws.ctrl + 2, nsub, ws.hit_t, ws.hit_obj, ws.hit_prim, sub_buf, counters,
                        ws.q2_pos, ws.q2, ws.ctrl + 5, (long)ws.slots);
     if (kDefer)
-        hipLaunchKernelGGL(k_wf_shadow_mesh<F>, g, dim3(kBlock), 0, st, sc, ws.s[nxt], (const int32_t*)ws.q2_pos,
-                           (const double*)ws.q2, (const uint32_t*)(ws.ctrl + 5), (long)ws.slots, ws.ctrl + 4);
+        hipLaunchKernelGGL(k_wf_shadow_mesh<F>, dim3(g_shadow), dim3(kBlock), 0, st, sc, ws.s[nxt],
+                           (const int32_t*)ws.q2_pos, (const double*)ws.q2, (const uint32_t*)(ws.ctrl + 5),
+                           ws.ctrl + 7, (long)ws.slots, ws.ctrl + 4, refill);
 }
 
 void launch_bounce(int features, dim3 g, hipStream_t st, const DevScene& sc, const RenderArgs& a, Workspace& ws,
@@ -309,13 +449,6 @@ void launch_bounce(int features, dim3 g, hipStream_t st, const DevScene& sc, con
         RT_WF_CASE(14) RT_WF_CASE(15)
     }
 #undef RT_WF_CASE
-}
-
-size_t env_size(const char* name, size_t dflt) {
-    const char* v = std::getenv(name);
-    if (!v || !*v) return dflt;
-    long long x = std::atoll(v);
-    return x > 0 ? (size_t)x : dflt;
 }
 
 }  // namespace

@@ -38,10 +38,11 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct Packed {
     std::vector<rt::DevObject> objects;
     std::vector<rt::DevMesh> meshes;
-    std::vector<rt::NodeMeta> meta;
-    std::vector<int32_t> child;
-    std::vector<double> box;
-    std::vector<int32_t> refs;
+    std::vector<int32_t> kids;   // [node][8]
+    std::vector<int2> up;        // [node]
+    std::vector<int2> leaves;    // [leaf] {first ltri, count}
+    std::vector<rt::DevTri> ltris;
+    std::vector<int32_t> ltri_id;
     std::vector<rt::DevTri> tris;
     std::vector<double> cum_area;
 };
@@ -81,10 +82,10 @@ void pack_scene(rt_scene* s) {
     const Scene& sc = s->host;
     for (const Mesh& m : sc.meshes) {
         rt::DevMesh dm{};
-        dm.node_base = (int32_t)p.meta.size();
+        dm.node_base = (int32_t)p.up.size();
         dm.n_nodes = (int32_t)m.octree.size();
-        dm.ref_base = (int32_t)p.refs.size();
-        dm.n_refs = (int32_t)m.octree.refs.size();
+        dm.root_leaf = -1;
+        dm.max_depth = (int32_t)m.octree.max_depth;
         dm.tri_base = (int32_t)p.tris.size();
         dm.n_tris = (int32_t)m.num_triangles();
         const Box& rb = m.octree.root;
@@ -124,22 +125,26 @@ void pack_scene(rt_scene* s) {
         }
         dm.total_weight = cum;
         const Octree& oc = m.octree;
+        // leaf ids in node order; leaf triangles copied in the leaf's own order
+        std::vector<int32_t> leaf_of(oc.size(), -1);
         for (size_t i = 0; i < oc.size(); ++i) {
-            rt::NodeMeta nm{};
-            nm.leaf_off = oc.kind[i] ? oc.leaf_off[i] + dm.ref_base : -1;
-            nm.leaf_cnt = oc.leaf_cnt[i];
-            nm.parent = oc.parent[i] >= 0 ? oc.parent[i] + dm.node_base : -1;
-            nm.slot = oc.slot[i];
-            p.meta.push_back(nm);
-            for (int k = 0; k < 8; ++k) {
-                int32_t c8 = oc.child[8 * i + k];
-                p.child.push_back(c8 >= 0 ? c8 + dm.node_base : -1);
+            if (!oc.kind[i]) continue;
+            leaf_of[i] = (int32_t)p.leaves.size();
+            p.leaves.push_back(int2{(int32_t)p.ltris.size(), oc.leaf_cnt[i]});
+            for (int32_t r = 0; r < oc.leaf_cnt[i]; ++r) {
+                const int32_t t = oc.refs[oc.leaf_off[i] + r];
+                p.ltris.push_back(p.tris[dm.tri_base + t]);
+                p.ltri_id.push_back(dm.tri_base + t);
             }
-            const Box& b = oc.box[i];
-            double bb[6] = {b.min.x, b.min.y, b.min.z, b.max.x, b.max.y, b.max.z};
-            p.box.insert(p.box.end(), bb, bb + 6);
         }
-        for (int32_t r : oc.refs) p.refs.push_back(r + dm.tri_base);
+        if (oc.size() > 0 && oc.kind[0]) dm.root_leaf = leaf_of[0];
+        for (size_t i = 0; i < oc.size(); ++i) {
+            p.up.push_back(int2{oc.parent[i] >= 0 ? oc.parent[i] + dm.node_base : -1, oc.slot[i]});
+            for (int k = 0; k < 8; ++k) {
+                const int32_t c8 = oc.child[8 * i + k];
+                p.kids.push_back(c8 < 0 ? rt::kKidEmpty : oc.kind[c8] ? rt::kid_leaf(leaf_of[c8]) : c8 + dm.node_base);
+            }
+        }
         p.meshes.push_back(dm);
     }
     for (const Object& o : sc.objects) {
@@ -214,13 +219,14 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
     if (!dc.ready) {
         const Packed& p = s->packed;
         std::vector<char> blob;
-        size_t o_obj, o_mesh, o_meta, o_child, o_box, o_refs, o_tris, o_cum;
+        size_t o_obj, o_mesh, o_kids, o_up, o_leaf, o_ltri, o_lid, o_tris, o_cum;
         put(blob, &o_obj, p.objects);
         put(blob, &o_mesh, p.meshes);
-        put(blob, &o_meta, p.meta);
-        put(blob, &o_child, p.child);
-        put(blob, &o_box, p.box);
-        put(blob, &o_refs, p.refs);
+        put(blob, &o_kids, p.kids);
+        put(blob, &o_up, p.up);
+        put(blob, &o_leaf, p.leaves);
+        put(blob, &o_ltri, p.ltris);
+        put(blob, &o_lid, p.ltri_id);
         put(blob, &o_tris, p.tris);
         put(blob, &o_cum, p.cum_area);
         void* d = nullptr;
@@ -234,10 +240,11 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         rt::DevScene ds{};
         ds.objects = (const rt::DevObject*)(b + o_obj);
         ds.meshes = (const rt::DevMesh*)(b + o_mesh);
-        ds.node_meta = (const rt::NodeMeta*)(b + o_meta);
-        ds.node_child = (const int32_t*)(b + o_child);
-        ds.node_box = (const double*)(b + o_box);
-        ds.tri_ref = (const int32_t*)(b + o_refs);
+        ds.node_kids = (const int32_t*)(b + o_kids);
+        ds.node_up = (const int2*)(b + o_up);
+        ds.leaf_span = (const int2*)(b + o_leaf);
+        ds.ltris = (const rt::DevTri*)(b + o_ltri);
+        ds.ltri_id = (const int32_t*)(b + o_lid);
         ds.tris = (const rt::DevTri*)(b + o_tris);
         ds.tri_cum_area = (const double*)(b + o_cum);
         ds.n_objects = (int32_t)p.objects.size();
