@@ -77,7 +77,7 @@ struct ShadowDefer {
 // trace), false when this sample's radiance ps.L is final. The shadow ray of next-event estimation
 // is traced inline.
 template <class C>
-RT_DEV bool shade_vertex(const DevScene& sc, LdsTab* tab, const RenderArgs& a, const SubPixel& sp, int smp, PathState& ps,
+RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, const SubPixel& sp, int smp, PathState& ps,
                          const HitRec& hr, ShadowDefer* defer = nullptr) {
     if (hr.obj < 0) return false;  // no hit: R = 0 (scene.rs:157, :175, :233)
     const DevObject& obj = sc.objects[hr.obj];
@@ -130,7 +130,7 @@ RT_DEV bool shade_vertex(const DevScene& sc, LdsTab* tab, const RenderArgs& a, c
                 double dist = mag(diff);
                 Ray sr{x, diff / dist};
                 const RayInv inv = make_inv(sr.d);
-                vis = visible_analytic<C>(sc, tab, sr, inv, dist) ? 1. : 0.;
+                vis = visible_analytic<C>(sc, sr, inv, dist) ? 1. : 0.;
                 if (vis > 0. && mesh_candidate<C>(sc, sr, inv, dist)) {
                     defer->pending = true;
                     defer->o = sr.o;
@@ -138,10 +138,10 @@ RT_DEV bool shade_vertex(const DevScene& sc, LdsTab* tab, const RenderArgs& a, c
                     defer->dist = dist;
                 }
             } else {
-                vis = visible<C>(sc, tab, x, y) ? 1. : 0.;
+                vis = visible<C>(sc, x, y) ? 1. : 0.;
             }
         } else {
-            vis = visible<C>(sc, tab, x, y) ? 1. : 0.;
+            vis = visible<C>(sc, x, y) ? 1. : 0.;
         }
         V3 c;
         if (!use_mis) {

@@ -535,34 +535,13 @@ struct Cfg {
     static constexpr bool compact = (F & 8) != 0;  // scene fits the compact tables (DevScene)
 };
 
-// Copies the compact tables (axis-plane coordinates, sphere centres and r^2) into LDS once per
-// workgroup: the trace loops then read them with broadcast ds_reads instead of holding ~56 SGPRs
-// (which spilled, and were restored with v_readlane bursts in every plane test).
-// RT_LDS_TABLES=1 reads the compact tables from LDS; the default keeps them in kernel arguments
-// (scalar registers), measured 26% faster on cornell_box (profiles/r01_variants.log).
-#ifndef RT_LDS_TABLES
-#define RT_LDS_TABLES 0
-#endif
-#if RT_LDS_TABLES
-#define RT_TAB_AX(K, i) tab[(K) * kMaxAxisPlanes + (i)]
-#define RT_TAB_SPH(i) (tab + kTabSph + 4 * (i))
-#else
-#define RT_TAB_AX(K, i) sc.ax_pos[K][i]
-#define RT_TAB_SPH(i) (sc.sph[i])
-#endif
-template <class C>
-RT_DEV LdsTab* stage_tables(const DevScene& sc, double* lds) {
-    if constexpr (C::compact && RT_LDS_TABLES) {
-        const int tid = threadIdx.x;
-        if (tid < kTabSize) {
-            double v;
-            if (tid < kTabSph) v = sc.ax_pos[tid / kMaxAxisPlanes][tid % kMaxAxisPlanes];
-            else v = sc.sph[(tid - kTabSph) / 4][(tid - kTabSph) % 4];
-            lds[tid] = v;
-        }
-        __syncthreads();
-    }
-    return (LdsTab*)lds;
+// Per-call view of the compact tables (scene_layout.h: CompactTab). The empty asm makes the pointer
+// opaque, so the scalar loads through it are issued inside each trace call instead of being
+// hoisted to the kernel entry, where the tables would hold ~100 SGPRs across the path loop.
+RT_DEV CTab* tables(const DevScene& sc) {
+    uint64_t p = (uint64_t)(uintptr_t)sc.ctab;
+    asm volatile("" : "+s"(p));
+    return (CTab*)p;
 }
 
 // One object's Geometry::intersect, reporting t (and the triangle for meshes).
@@ -601,8 +580,8 @@ RT_DEV bool sphere_c(P c, const Ray& ray, double* tout) {
 }
 // Axis planes of axis K: one |d_K| test and one reciprocal serve all of them (plane_t's axis path).
 template <int K, class Visit>
-RT_DEV void axis_planes(const DevScene& sc, LdsTab* tab, const Ray& ray, const RayInv& inv, Visit&& visit) {
-    const int n = sc.n_ax[K];
+RT_DEV void axis_planes(const DevScene& sc, CTab* T, const Ray& ray, const RayInv& inv, Visit&& visit) {
+    const int n = T->n_ax[K];
     if (n == 0) return;
     const double dk = K == 0 ? ray.d.x : K == 1 ? ray.d.y : ray.d.z;
     if (fabs(dk) < 0.0001) return;
@@ -610,29 +589,30 @@ RT_DEV void axis_planes(const DevScene& sc, LdsTab* tab, const Ray& ray, const R
 #pragma unroll
     for (int i = 0; i < kMaxAxisPlanes; ++i) {
         if (i < n) {
-            double num = RT_TAB_AX(K, i) - ok;
+            double num = T->ax_pos[K][i] - ok;
             double t = K == 0 ? div_x(num, ray, inv) : K == 1 ? div_y(num, ray, inv) : div_z(num, ray, inv);
-            if (t >= 0.) visit(t, sc.ax_idx[K][i], -1);
+            if (t >= 0.) visit(t, T->ax_idx[K][i], -1);
         }
     }
 }
 
 template <class C>
-RT_DEV HitRec trace_closest(const DevScene& sc, LdsTab* tab, const Ray& ray) {
+RT_DEV HitRec trace_closest(const DevScene& sc, const Ray& ray) {
+    CTab* T = tables(sc);
     HitRec h{0.0, -1, -1};
     const RayInv inv = make_inv(ray.d);
     if constexpr (C::compact) {
         auto visit = [&](double t, int idx, int prim) { consider(h, t, idx, prim); };
-        axis_planes<0>(sc, tab, ray, inv, visit);
-        axis_planes<1>(sc, tab, ray, inv, visit);
-        axis_planes<2>(sc, tab, ray, inv, visit);
+        axis_planes<0>(sc, T, ray, inv, visit);
+        axis_planes<1>(sc, T, ray, inv, visit);
+        axis_planes<2>(sc, T, ray, inv, visit);
 #pragma unroll
         for (int i = 0; i < kMaxSpheres; ++i) {
             double t;
-            if (i < sc.n_sph && sphere_c(RT_TAB_SPH(i), ray, &t)) consider(h, t, sc.sph_idx[i], -1);
+            if (i < T->n_sph && sphere_c(T->sph[i], ray, &t)) consider(h, t, T->sph_idx[i], -1);
         }
-        for (int i = 0; i < sc.n_gen; ++i) {
-            const int idx = sc.gen_idx[i];
+        for (int i = 0; i < T->n_gen; ++i) {
+            const int idx = T->gen_idx[i];
             double t;
             int prim = -1;
             const double tmax = h.obj >= 0 ? h.t : INFINITY;
@@ -677,7 +657,8 @@ RT_DEV void surface(const DevScene& sc, const Ray& ray, const HitRec& h, V3* pos
 // intersect t satisfies t + 0.001 < |y - x| (equivalent to the nearest-hit test because x + 0.001
 // rounds monotonically). Analytic objects are tested before meshes (order-free for a boolean).
 template <class C>
-RT_DEV bool visible(const DevScene& sc, LdsTab* tab, V3 x, V3 y) {
+RT_DEV bool visible(const DevScene& sc, V3 x, V3 y) {
+    CTab* T = tables(sc);
     const double ERR_MARGIN = 0.001;
     V3 diff = y - x;
     double dist = mag(diff);
@@ -686,19 +667,19 @@ RT_DEV bool visible(const DevScene& sc, LdsTab* tab, V3 x, V3 y) {
     if constexpr (C::compact) {
         bool occluded = false;
         auto visit = [&](double t, int, int) { occluded |= !(t + ERR_MARGIN >= dist); };
-        axis_planes<0>(sc, tab, r, inv, visit);
-        axis_planes<1>(sc, tab, r, inv, visit);
-        axis_planes<2>(sc, tab, r, inv, visit);
+        axis_planes<0>(sc, T, r, inv, visit);
+        axis_planes<1>(sc, T, r, inv, visit);
+        axis_planes<2>(sc, T, r, inv, visit);
 #pragma unroll
         for (int i = 0; i < kMaxSpheres; ++i) {
             double t;
-            if (i < sc.n_sph && sphere_c(RT_TAB_SPH(i), r, &t)) occluded |= !(t + ERR_MARGIN >= dist);
+            if (i < T->n_sph && sphere_c(T->sph[i], r, &t)) occluded |= !(t + ERR_MARGIN >= dist);
         }
         if (occluded) return false;
-        for (int i = 0; i < sc.n_gen; ++i) {
+        for (int i = 0; i < T->n_gen; ++i) {
             double t;
             int prim;
-            if (object_t<C>(sc, sc.objects[sc.gen_idx[i]], r, inv, &t, &prim, dist) && !(t + ERR_MARGIN >= dist))
+            if (object_t<C>(sc, sc.objects[T->gen_idx[i]], r, inv, &t, &prim, dist) && !(t + ERR_MARGIN >= dist))
                 return false;
         }
         return true;
@@ -718,19 +699,20 @@ RT_DEV bool visible(const DevScene& sc, LdsTab* tab, V3 x, V3 y) {
 // ---- pieces of trace_ray / mutually_visible for the wavefront's deferred mesh queries ----
 // (compact scenes only: analytic objects = axis planes, spheres, and non-mesh generic objects)
 template <class C>
-RT_DEV HitRec trace_analytic(const DevScene& sc, LdsTab* tab, const Ray& ray, const RayInv& inv) {
+RT_DEV HitRec trace_analytic(const DevScene& sc, const Ray& ray, const RayInv& inv) {
+    CTab* T = tables(sc);
     HitRec h{0.0, -1, -1};
     auto visit = [&](double t, int idx, int prim) { consider(h, t, idx, prim); };
-    axis_planes<0>(sc, tab, ray, inv, visit);
-    axis_planes<1>(sc, tab, ray, inv, visit);
-    axis_planes<2>(sc, tab, ray, inv, visit);
+    axis_planes<0>(sc, T, ray, inv, visit);
+    axis_planes<1>(sc, T, ray, inv, visit);
+    axis_planes<2>(sc, T, ray, inv, visit);
 #pragma unroll
     for (int i = 0; i < kMaxSpheres; ++i) {
         double t;
-        if (i < sc.n_sph && sphere_c(RT_TAB_SPH(i), ray, &t)) consider(h, t, sc.sph_idx[i], -1);
+        if (i < T->n_sph && sphere_c(T->sph[i], ray, &t)) consider(h, t, T->sph_idx[i], -1);
     }
-    for (int i = 0; i < sc.n_gen; ++i) {
-        const int idx = sc.gen_idx[i];
+    for (int i = 0; i < T->n_gen; ++i) {
+        const int idx = T->gen_idx[i];
         const DevObject& o = sc.objects[idx];
         double t;
         int prim = -1;
@@ -741,8 +723,9 @@ RT_DEV HitRec trace_analytic(const DevScene& sc, LdsTab* tab, const Ray& ray, co
 // Adds the meshes' hits to an analytic closest hit (Scene::trace_ray's loop over the mesh objects).
 template <class C>
 RT_DEV void trace_meshes(const DevScene& sc, const Ray& ray, const RayInv& inv, HitRec& h) {
-    for (int i = 0; i < sc.n_gen; ++i) {
-        const int idx = sc.gen_idx[i];
+    CTab* T = tables(sc);
+    for (int i = 0; i < T->n_gen; ++i) {
+        const int idx = T->gen_idx[i];
         const DevObject& o = sc.objects[idx];
         if (o.geom != GEOM_MESH) continue;
         double t;
@@ -753,9 +736,10 @@ RT_DEV void trace_meshes(const DevScene& sc, const Ray& ray, const RayInv& inv, 
 // Could any mesh change this ray's result (closest hit so far at tmax / shadow distance tmax)?
 template <class C>
 RT_DEV bool mesh_candidate(const DevScene& sc, const Ray& ray, const RayInv& inv, double tmax) {
+    CTab* T = tables(sc);
     bool any = false;
-    for (int i = 0; i < sc.n_gen; ++i) {
-        const DevObject& o = sc.objects[sc.gen_idx[i]];
+    for (int i = 0; i < T->n_gen; ++i) {
+        const DevObject& o = sc.objects[T->gen_idx[i]];
         if (o.geom == GEOM_MESH && sc.meshes[o.mesh].n_nodes > 0) {
             const DevMesh& m = sc.meshes[o.mesh];
             any |= near_box(m.root_box, ray, inv, m.cull_pad, tmax);
@@ -765,21 +749,22 @@ RT_DEV bool mesh_candidate(const DevScene& sc, const Ray& ray, const RayInv& inv
 }
 // mutually_visible split: the analytic objects here, the meshes later (mesh_occludes).
 template <class C>
-RT_DEV bool visible_analytic(const DevScene& sc, LdsTab* tab, const Ray& r, const RayInv& inv, double dist) {
+RT_DEV bool visible_analytic(const DevScene& sc, const Ray& r, const RayInv& inv, double dist) {
+    CTab* T = tables(sc);
     const double ERR_MARGIN = 0.001;
     bool occluded = false;
     auto visit = [&](double t, int, int) { occluded |= !(t + ERR_MARGIN >= dist); };
-    axis_planes<0>(sc, tab, r, inv, visit);
-    axis_planes<1>(sc, tab, r, inv, visit);
-    axis_planes<2>(sc, tab, r, inv, visit);
+    axis_planes<0>(sc, T, r, inv, visit);
+    axis_planes<1>(sc, T, r, inv, visit);
+    axis_planes<2>(sc, T, r, inv, visit);
 #pragma unroll
     for (int i = 0; i < kMaxSpheres; ++i) {
         double t;
-        if (i < sc.n_sph && sphere_c(RT_TAB_SPH(i), r, &t)) occluded |= !(t + ERR_MARGIN >= dist);
+        if (i < T->n_sph && sphere_c(T->sph[i], r, &t)) occluded |= !(t + ERR_MARGIN >= dist);
     }
     if (occluded) return false;
-    for (int i = 0; i < sc.n_gen; ++i) {
-        const DevObject& o = sc.objects[sc.gen_idx[i]];
+    for (int i = 0; i < T->n_gen; ++i) {
+        const DevObject& o = sc.objects[T->gen_idx[i]];
         double t;
         int prim;
         if (o.geom != GEOM_MESH && object_t<C>(sc, o, r, inv, &t, &prim, dist) && !(t + ERR_MARGIN >= dist)) return false;
@@ -788,9 +773,10 @@ RT_DEV bool visible_analytic(const DevScene& sc, LdsTab* tab, const Ray& r, cons
 }
 template <class C>
 RT_DEV bool mesh_occludes(const DevScene& sc, const Ray& r, const RayInv& inv, double dist) {
+    CTab* T = tables(sc);
     const double ERR_MARGIN = 0.001;
-    for (int i = 0; i < sc.n_gen; ++i) {
-        const DevObject& o = sc.objects[sc.gen_idx[i]];
+    for (int i = 0; i < T->n_gen; ++i) {
+        const DevObject& o = sc.objects[T->gen_idx[i]];
         if (o.geom != GEOM_MESH) continue;
         double t;
         int prim;

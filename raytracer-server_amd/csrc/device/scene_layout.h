@@ -65,8 +65,20 @@ struct DevTri {
 constexpr int kMaxAxisPlanes = 4;  // per axis
 constexpr int kMaxSpheres = 4;
 constexpr int kMaxGeneric = 8;     // meshes and non-axis planes
-constexpr int kTabSph = 3 * kMaxAxisPlanes;          // LDS table: axis-plane coordinates, then
-constexpr int kTabSize = kTabSph + 4 * kMaxSpheres;  //   sphere (centre xyz, r^2)
+// The compact tables live in device memory (part of the scene blob) and are read through a
+// constant-address-space pointer: scalar loads at each use, so they never occupy SGPRs across the
+// path loop (as kernel arguments they did, and the spilled SGPRs were reloaded with ~900 static
+// v_readlane instructions in the cornell megakernel).
+struct CompactTab {
+    int32_t n_ax[3];                         // planes with n = +-e_k, per axis k
+    int32_t n_sph, n_gen, pad;
+    int32_t ax_idx[3][kMaxAxisPlanes];
+    double ax_pos[3][kMaxAxisPlanes];        // plane point coordinate along its axis
+    int32_t sph_idx[kMaxSpheres];
+    double sph[kMaxSpheres][4];              // centre xyz, r*r
+    int32_t gen_idx[kMaxGeneric];            // everything else, through the generic intersector
+};
+typedef const __attribute__((address_space(4))) CompactTab CTab;
 
 struct DevScene {
     const DevObject* objects;
@@ -79,21 +91,9 @@ struct DevScene {
     const int32_t* ltri_id;     // [ltri] global triangle index (the hit's `prim`)
     const DevTri* tris;         // per triangle (surface normal, mesh-light sampling)
     const double* tri_cum_area;  // per triangle, cumulative area within its mesh (mesh-light pick)
-    int32_t n_objects, light, n_meshes, mesh_order_last;  // mesh_order_last: test meshes after analytic objects
+    const CompactTab* ctab;     // compact tables (valid when `compact`; see Cfg::compact)
+    int32_t n_objects, light, n_meshes, compact;
     double cam_pos[3], cam_dir[3];
-    // compact tables (valid when `compact`; see Cfg::compact)
-    int32_t compact;
-    int32_t n_ax[3];                         // planes with n = +-e_k, per axis k
-    int32_t n_sph, n_gen;
-    int32_t ax_idx[3][kMaxAxisPlanes];
-    double ax_pos[3][kMaxAxisPlanes];        // plane point coordinate along its axis
-    int32_t sph_idx[kMaxSpheres];
-    double sph[kMaxSpheres][4];              // centre xyz, r*r
-    int32_t gen_idx[kMaxGeneric];            // everything else, through the generic intersector
 };
-
-// LDS-resident copy of the compact tables (ax_pos, then sph), typed in the LDS address space so
-// reads compile to ds_read (a generic pointer would become flat_load).
-typedef const __attribute__((address_space(3))) double LdsTab;
 
 }  // namespace rt

@@ -38,8 +38,6 @@ template <int F, int W>
 __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
                                                           uint32_t* next_sub, long nsub) {
     using C = Cfg<F>;
-    __shared__ double s_tab[kTabSize];
-    LdsTab* tab = stage_tables<C>(sc, s_tab);
     const int lane = threadIdx.x & 63;
     unsigned long long nverts = 0;
     long id = wave_ticket(next_sub, true);
@@ -53,9 +51,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
         bool done = false;
         if (active) {
             if (fresh) begin_sample(sc, a, sp, s, ps);
-            HitRec hr = trace_closest<C>(sc, tab, ps.ray);
+            HitRec hr = trace_closest<C>(sc, ps.ray);
             nverts += hr.obj >= 0;
-            fresh = !shade_vertex<C>(sc, tab, a, sp, s, ps, hr);
+            fresh = !shade_vertex<C>(sc, a, sp, s, ps, hr);
             if (fresh) {
                 acc = acc + ps.L * a.inv_n;  // server.rs:357-358
                 if (++s == a.n_samples) {
@@ -69,6 +67,153 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
         }
         // cancellation (RenderJob::stop, server.rs:201-203): checked when a lane would start a new
         // subpixel; a set flag stops handing out work, lanes finish the subpixel they hold
+        bool stop = false;
+        if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+        long nid = wave_ticket(next_sub, done && !stop);
+        if (done) {
+            id = stop ? nsub : nid;
+            active = id < nsub;
+            if (active) sp = subpixel_of(a, id);
+            acc = v3(0, 0, 0);
+            s = 0;
+            fresh = true;
+        }
+    }
+    if (a.counters) {
+        unsigned long long v = nverts;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (lane == 0 && v) atomicAdd(a.counters, v);
+    }
+}
+
+// Begins the octree walk of the next candidate mesh after gen slot g (Scene::trace_ray's /
+// mutually_visible's loop over the mesh objects); false when no mesh is left.
+template <class C>
+RT_DEV bool next_mesh_walk(const DevScene& sc, const Ray& r, const RayInv& inv, double tmax, int& g, int& mi,
+                           OctWalk& w) {
+    for (++g; g < tables(sc)->n_gen; ++g) {
+        const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
+        if (o.geom == GEOM_MESH && walk_begin(sc, sc.meshes[o.mesh], r, inv, tmax, w)) {
+            mi = o.mesh;
+            return true;
+        }
+    }
+    return false;
+}
+
+// Megakernel for scenes with triangle meshes: octree walks interleaved with path vertices.
+// A walk is long-tailed (tens of steps for the few rays that reach the mesh's box; none for the
+// rest), so tracing it to completion inside the vertex makes every lane of the wave wait for the
+// wave's longest walk. Here a lane whose ray needs a mesh walk parks its path and walks
+// `ksteps` steps per iteration (walk_step is resumable), while the other lanes of the wave keep
+// shading vertices; a lane rejoins the vertex work the iteration its walk ends. The walk queries
+// are the wavefront's deferred ones (closest: the analytic hit, then the meshes in gen order with
+// the reference's tie rule; shadow: the analytic objects let the ray through, then any mesh may
+// block it), so every path produces the same bits as k_megakernel_f64 (tested).
+enum : int { PH_TRACE = 0, PH_WALK_CLOSEST = 1, PH_WALK_SHADOW = 2 };
+template <int F, int W>
+__global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
+                                                               uint32_t* next_sub, long nsub, int ksteps) {
+    using C = Cfg<F>;
+    static_assert(C::mesh && C::compact, "mesh megakernel needs the compact tables");
+    const int lane = threadIdx.x & 63;
+    unsigned long long nverts = 0;
+    long id = wave_ticket(next_sub, true);
+    bool active = id < nsub;
+    SubPixel sp = subpixel_of(a, active ? id : 0);
+    V3 acc = v3(0, 0, 0);
+    int s = 0;
+    PathState ps;
+    bool fresh = true;
+    // walk state: the walked ray (ps.ray for a closest query, the shadow ray for a shadow query)
+    int phase = PH_TRACE;
+    bool walking = false, occluded = false, cont = false;
+    Ray wr;
+    RayInv wi;
+    double wdist = 0.0;         // shadow: |y - x|
+    HitRec h{0.0, -1, -1};      // closest: analytic hit merged with the finished mesh walks
+    V3 wc = v3(0, 0, 0);        // shadow: the pending NEE term (already weighted by beta)
+    int g = -1, mi = 0;         // gen slot and mesh being walked
+    OctWalk w;
+    while (__any(active)) {
+        for (int k = 0; k < ksteps && __any(walking); ++k) {
+            if (walking) {
+                double t;
+                int prim;
+                const int st = walk_step(sc, sc.meshes[mi], wr, wi, w, &t, &prim);
+                if (st != WALK_RUN) {
+                    bool fin;
+                    if (phase == PH_WALK_CLOSEST) {
+                        if (st == WALK_HIT) consider(h, t, tables(sc)->gen_idx[g], prim);
+                        fin = !next_mesh_walk<C>(sc, wr, wi, h.obj >= 0 ? h.t : INFINITY, g, mi, w);
+                    } else {
+                        occluded = st == WALK_HIT && !(t + 0.001 >= wdist);  // mutually_visible's ERR_MARGIN
+                        fin = occluded || !next_mesh_walk<C>(sc, wr, wi, wdist, g, mi, w);
+                    }
+                    walking = !fin;
+                }
+            }
+        }
+        bool done = false;
+        if (active && !walking) {
+            bool shade_now = false, sample_end = false;
+            if (phase == PH_WALK_SHADOW) {
+                if (!occluded) ps.L = ps.L + wc;
+                phase = PH_TRACE;
+                sample_end = !cont;
+            } else if (phase == PH_WALK_CLOSEST) {
+                shade_now = true;
+            } else {
+                if (fresh) {
+                    begin_sample(sc, a, sp, s, ps);
+                    fresh = false;
+                }
+                wr = ps.ray;
+                wi = make_inv(wr.d);
+                h = trace_analytic<C>(sc, wr, wi);
+                g = -1;
+                if (next_mesh_walk<C>(sc, wr, wi, h.obj >= 0 ? h.t : INFINITY, g, mi, w)) {
+                    phase = PH_WALK_CLOSEST;
+                    walking = true;
+                } else {
+                    shade_now = true;
+                }
+            }
+            if (shade_now) {
+                nverts += h.obj >= 0;
+                ShadowDefer df;
+                df.pending = false;
+                cont = shade_vertex<C>(sc, a, sp, s, ps, h, &df);
+                phase = PH_TRACE;
+                if (df.pending) {
+                    wr = Ray{df.o, df.d};
+                    wi = make_inv(wr.d);
+                    wdist = df.dist;
+                    wc = df.c;
+                    g = -1;
+                    occluded = false;
+                    if (next_mesh_walk<C>(sc, wr, wi, wdist, g, mi, w)) {
+                        phase = PH_WALK_SHADOW;
+                        walking = true;
+                    } else {
+                        ps.L = ps.L + wc;
+                    }
+                }
+                if (!walking) sample_end = !cont;
+            }
+            if (sample_end) {
+                acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                fresh = true;
+                if (++s == a.n_samples) {
+                    double* o = sub_buf + (size_t)id * 3;
+                    o[0] = acc.x;
+                    o[1] = acc.y;
+                    o[2] = acc.z;
+                    done = true;
+                }
+            }
+        }
         bool stop = false;
         if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
         long nid = wave_ticket(next_sub, done && !stop);
@@ -110,12 +255,10 @@ __global__ __launch_bounds__(256) void k_finalize_f64(RenderArgs a, const double
 __global__ __launch_bounds__(256) void k_trace_f64(DevScene sc, long n, const double* __restrict__ o,
                                                    const double* __restrict__ d, double* t, int32_t* obj,
                                                    double* pos, double* nrm) {
-    __shared__ double s_tab[kTabSize];
-    LdsTab* tab = stage_tables<Cfg<9>>(sc, s_tab);
     long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Ray r{v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2])};
-    HitRec h = sc.compact ? trace_closest<Cfg<9>>(sc, tab, r) : trace_closest<Cfg<1>>(sc, tab, r);
+    HitRec h = sc.compact ? trace_closest<Cfg<9>>(sc, r) : trace_closest<Cfg<1>>(sc, r);
     obj[i] = h.obj;
     t[i] = h.obj >= 0 ? h.t : 0.0;
     if (h.obj >= 0) {
@@ -144,6 +287,36 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double
     hipError_t e = hipMemsetAsync(next_sub, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     dim3 g((unsigned)blocks), b(256);
+    // mesh scenes with compact tables and an octree of at least RT_MK_INTERLEAVE nodes: interleaved
+    // walks (0 selects the fused per-vertex traversal for A/B runs); RT_MK_KSTEPS walk steps per
+    // vertex iteration
+    static const int interleave = [] {
+        const char* v = std::getenv("RT_MK_INTERLEAVE");
+        return v ? std::atoi(v) : 64;
+    }();
+    static const int ksteps = [] {
+        const char* v = std::getenv("RT_MK_KSTEPS");
+        return v ? std::max(1, std::atoi(v)) : 8;
+    }();
+    static const int mwaves = [] {
+        const char* v = std::getenv("RT_MK_MESH_WAVES");
+        return v ? std::atoi(v) : 2;
+    }();
+    // shallow octrees (cubes: 9 nodes) walk in a few steps: the fused traversal is faster there
+    // (profiles/r01_interleave_ab.log)
+    if (interleave && (a.features & 9) == 9 && a.mesh_nodes >= interleave) {
+        const long mres = (long)ncu * (mwaves == 4 ? 4 : 2);
+        const long mblocks = std::max(1L, std::min(mres, (nsub + 255) / 256));
+        dim3 mg((unsigned)mblocks);
+#define RT_MM_CASE(F)                                                                                                  \
+    case F:                                                                                                            \
+        if (mwaves == 4) hipLaunchKernelGGL((k_megakernel_mesh_f64<F, 4>), mg, b, 0, st, sc, a, sub_buf, next_sub, nsub, ksteps); \
+        else hipLaunchKernelGGL((k_megakernel_mesh_f64<F, 2>), mg, b, 0, st, sc, a, sub_buf, next_sub, nsub, ksteps);            \
+        break;
+        switch (a.features & 15) { RT_MM_CASE(9) RT_MM_CASE(11) RT_MM_CASE(13) RT_MM_CASE(15) }
+#undef RT_MM_CASE
+        return hipGetLastError();
+    }
 #define RT_MK_CASE(F)                                                                                  \
     case F:                                                                                            \
         if (waves == 4) hipLaunchKernelGGL((k_megakernel_f64<F, 4>), g, b, 0, st, sc, a, sub_buf, next_sub, nsub); \

@@ -116,8 +116,6 @@ __global__ __launch_bounds__(kBlock) void k_wf_extend(DevScene sc, PathStream A,
                                                        uint32_t* heads) {
     using C = Cfg<F>;
     constexpr bool kDefer = C::mesh && C::compact;
-    __shared__ double s_tab[kTabSize];
-    LdsTab* tab = stage_tables<C>(sc, s_tab);
     const long n = (long)*cnt_in;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         *cnt_out = 0;  // stream B is refilled by k_wf_shade
@@ -135,13 +133,13 @@ __global__ __launch_bounds__(kBlock) void k_wf_extend(DevScene sc, PathStream A,
                 hobj[i] = -2;
             } else if constexpr (kDefer) {
                 const RayInv inv = make_inv(r.d);
-                HitRec h = trace_analytic<C>(sc, tab, r, inv);
+                HitRec h = trace_analytic<C>(sc, r, inv);
                 ht[i] = h.t;
                 hobj[i] = h.obj;
                 hprim[i] = h.prim;
                 cand = mesh_candidate<C>(sc, r, inv, h.obj >= 0 ? h.t : INFINITY);
             } else {
-                HitRec h = trace_closest<C>(sc, tab, r);
+                HitRec h = trace_closest<C>(sc, r);
                 ht[i] = h.t;
                 hobj[i] = h.obj;
                 hprim[i] = h.prim;
@@ -217,7 +215,7 @@ struct ClosestQuery {
     Ray ray;
     RayInv inv;
     HitRec h;
-    int g;  // position in sc.gen_idx of the mesh being walked
+    int g;  // position in the gen_idx table of the mesh being walked
     OctWalk w;
     RT_DEV bool start(uint32_t qi) {
         i = q1[qi];
@@ -227,17 +225,17 @@ struct ClosestQuery {
         g = -1;
         return true;
     }
-    RT_DEV int mesh() const { return sc.objects[sc.gen_idx[g]].mesh; }
+    RT_DEV int mesh() const { return sc.objects[tables(sc)->gen_idx[g]].mesh; }
     RT_DEV bool next_mesh() {
-        for (++g; g < sc.n_gen; ++g) {
-            const DevObject& o = sc.objects[sc.gen_idx[g]];
+        for (++g; g < tables(sc)->n_gen; ++g) {
+            const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
             if (o.geom == GEOM_MESH && walk_begin(sc, sc.meshes[o.mesh], ray, inv, h.obj >= 0 ? h.t : INFINITY, w))
                 return true;
         }
         return false;
     }
     RT_DEV bool hit(double t, int prim) {
-        consider(h, t, sc.gen_idx[g], prim);
+        consider(h, t, tables(sc)->gen_idx[g], prim);
         return false;
     }
     RT_DEV void finish() {
@@ -279,10 +277,10 @@ struct ShadowQuery {
         g = -1;
         return true;
     }
-    RT_DEV int mesh() const { return sc.objects[sc.gen_idx[g]].mesh; }
+    RT_DEV int mesh() const { return sc.objects[tables(sc)->gen_idx[g]].mesh; }
     RT_DEV bool next_mesh() {
-        for (++g; g < sc.n_gen; ++g) {
-            const DevObject& o = sc.objects[sc.gen_idx[g]];
+        for (++g; g < tables(sc)->n_gen; ++g) {
+            const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
             if (o.geom == GEOM_MESH && walk_begin(sc, sc.meshes[o.mesh], ray, inv, dist, w)) return true;
         }
         return false;
@@ -319,8 +317,6 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, 
                                                       double* __restrict__ q2, uint32_t* q2_cnt, long slots) {
     using C = Cfg<F>;
     constexpr bool kDefer = C::mesh && C::compact;
-    __shared__ double s_tab[kTabSize];
-    LdsTab* tab = stage_tables<C>(sc, s_tab);
     const long n = (long)*cnt_in;
     const long stride = (long)gridDim.x * blockDim.x;
     const bool mis = a.mis != 0;
@@ -343,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, 
             } else {
                 HitRec hr{ht[i], hobj[i], hprim[i]};
                 nverts += hr.obj >= 0;
-                emit = shade_vertex<C>(sc, tab, a, sp, smp, ps, hr, kDefer ? &sd : nullptr);
+                emit = shade_vertex<C>(sc, a, sp, smp, ps, hr, kDefer ? &sd : nullptr);
                 finished = !emit;
                 if (finished && sd.pending) {
                     ps.kind = K_DONE;  // keep the path one more bounce for its shadow result

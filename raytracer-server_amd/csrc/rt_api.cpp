@@ -176,7 +176,7 @@ void pack_scene(rt_scene* s) {
 }
 
 // Groups objects for the compact trace (axis planes per axis, spheres, everything else).
-void fill_compact(const Packed& p, rt::DevScene* ds) {
+void fill_compact(const Packed& p, rt::CompactTab* ds, int32_t* compact) {
     int nax[3] = {0, 0, 0}, ns = 0, ng = 0;
     bool ok = true;
     for (size_t i = 0; i < p.objects.size(); ++i) {
@@ -199,7 +199,7 @@ void fill_compact(const Packed& p, rt::DevScene* ds) {
             ds->gen_idx[ng++] = (int32_t)i;
         }
     }
-    ds->compact = ok ? 1 : 0;
+    *compact = ok ? 1 : 0;
     for (int k = 0; k < 3; ++k) ds->n_ax[k] = ok ? nax[k] : 0;
     ds->n_sph = ok ? ns : 0;
     ds->n_gen = ok ? ng : 0;
@@ -219,7 +219,12 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
     if (!dc.ready) {
         const Packed& p = s->packed;
         std::vector<char> blob;
-        size_t o_obj, o_mesh, o_kids, o_up, o_leaf, o_ltri, o_lid, o_tris, o_cum;
+        size_t o_obj, o_mesh, o_kids, o_up, o_leaf, o_ltri, o_lid, o_tris, o_cum, o_tab;
+        std::vector<rt::CompactTab> tab(1);
+        std::memset(tab.data(), 0, sizeof(rt::CompactTab));
+        int32_t compact = 0;
+        fill_compact(p, tab.data(), &compact);
+        put(blob, &o_tab, tab);
         put(blob, &o_obj, p.objects);
         put(blob, &o_mesh, p.meshes);
         put(blob, &o_kids, p.kids);
@@ -248,7 +253,8 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.tris = (const rt::DevTri*)(b + o_tris);
         ds.tri_cum_area = (const double*)(b + o_cum);
         ds.n_objects = (int32_t)p.objects.size();
-        fill_compact(p, &ds);
+        ds.ctab = (const rt::CompactTab*)(b + o_tab);
+        ds.compact = compact;
         ds.light = s->host.light;
         ds.n_meshes = (int32_t)p.meshes.size();
         cp3(ds.cam_pos, s->host.cam_pos);
@@ -311,6 +317,7 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
         bool phong = false;
         for (const auto& o : s->host.objects) phong |= o.brdf == RT_BRDF_PHONG;
         a.features = (s->host.meshes.empty() ? 0 : 1) | (phong ? 2 : 0) | (a.mis ? 4 : 0) | (ds.compact ? 8 : 0);
+        for (const auto& m : s->host.meshes) a.mesh_nodes = std::max(a.mesh_nodes, (int32_t)m.octree.size());
     }
     a.seed = p->seed;
     rt::host::camera_frame(s->host, p->width, p->height, a.cx, a.cy);
