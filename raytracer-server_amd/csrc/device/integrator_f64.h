@@ -37,11 +37,13 @@ struct SubPixel {
     int col, yref, sx, sy, sub;
 };
 RT_DEV SubPixel subpixel_of(const RenderArgs& a, long p) {
-    long pix = p >> 2;
+    const uint32_t pix = (uint32_t)(p >> 2);  // < width * height < 2^32 (rt_api.cpp: check_params)
+    const uint32_t tw = (uint32_t)a.tw;
+    const uint32_t r = pix / tw;
     SubPixel s;
     s.sub = (int)(p & 3);
-    s.col = a.x0 + (int)(pix % a.tw);
-    int row = a.y0 + (int)(pix / a.tw);
+    s.col = a.x0 + (int)(pix - r * tw);
+    int row = a.y0 + (int)r;
     s.yref = a.height - row - 1;
     s.pid = (uint32_t)row * (uint32_t)a.width + (uint32_t)s.col;
     s.sx = s.sub & 1;
@@ -77,7 +79,7 @@ struct ShadowDefer {
 // trace), false when this sample's radiance ps.L is final. The shadow ray of next-event estimation
 // is traced inline.
 template <class C>
-RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, const SubPixel& sp, int smp, PathState& ps,
+RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
                          const HitRec& hr, ShadowDefer* defer = nullptr) {
     if (hr.obj < 0) return false;  // no hit: R = 0 (scene.rs:157, :175, :233)
     const DevObject& obj = sc.objects[hr.obj];

@@ -28,6 +28,16 @@ __device__ __forceinline__ long wave_ticket(uint32_t* counter, bool want) {
     return want ? (long)base + __popcll(below) : -1;
 }
 
+// Adds the wave's vertex counts to *counter and zeroes them. All 64 lanes must call it together.
+__device__ __forceinline__ void flush_count(unsigned long long* counter, uint32_t& n) {
+    if (!counter) return;
+    unsigned long long v = n;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (__lane_id() == 0 && v) atomicAdd(counter, v);
+    n = 0;
+}
+
 // Persistent megakernel: a resident grid whose lanes pull subpixels from a global counter. A lane
 // walks the spp/4 sample paths of its subpixel vertex by vertex; when a path ends, the next sample
 // starts in the same iteration (regeneration); when the subpixel is done its mean goes to
@@ -38,11 +48,9 @@ template <int F, int W>
 __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
                                                           uint32_t* next_sub, long nsub) {
     using C = Cfg<F>;
-    const int lane = threadIdx.x & 63;
-    unsigned long long nverts = 0;
+    uint32_t nverts = 0;
     long id = wave_ticket(next_sub, true);
     bool active = id < nsub;
-    SubPixel sp = subpixel_of(a, active ? id : 0);
     V3 acc = v3(0, 0, 0);
     int s = 0;
     PathState ps;
@@ -50,10 +58,10 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
     while (__any(active)) {
         bool done = false;
         if (active) {
-            if (fresh) begin_sample(sc, a, sp, s, ps);
+            if (fresh) begin_sample(sc, a, subpixel_of(a, id), s, ps);
             HitRec hr = trace_closest<C>(sc, ps.ray);
             nverts += hr.obj >= 0;
-            fresh = !shade_vertex<C>(sc, a, sp, s, ps, hr);
+            fresh = !shade_vertex<C>(sc, a, ps, hr);
             if (fresh) {
                 acc = acc + ps.L * a.inv_n;  // server.rs:357-358
                 if (++s == a.n_samples) {
@@ -70,21 +78,16 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
         bool stop = false;
         if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
         long nid = wave_ticket(next_sub, done && !stop);
+        if (__any(done)) flush_count(a.counters, nverts);  // keeps the 32-bit lane counts far from overflow
         if (done) {
             id = stop ? nsub : nid;
             active = id < nsub;
-            if (active) sp = subpixel_of(a, id);
             acc = v3(0, 0, 0);
             s = 0;
             fresh = true;
         }
     }
-    if (a.counters) {
-        unsigned long long v = nverts;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        if (lane == 0 && v) atomicAdd(a.counters, v);
-    }
+    flush_count(a.counters, nverts);
 }
 
 // Begins the octree walk of the next candidate mesh after gen slot g (Scene::trace_ray's /
@@ -117,11 +120,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, Ren
                                                                uint32_t* next_sub, long nsub, int ksteps) {
     using C = Cfg<F>;
     static_assert(C::mesh && C::compact, "mesh megakernel needs the compact tables");
-    const int lane = threadIdx.x & 63;
-    unsigned long long nverts = 0;
+    uint32_t nverts = 0;
     long id = wave_ticket(next_sub, true);
     bool active = id < nsub;
-    SubPixel sp = subpixel_of(a, active ? id : 0);
     V3 acc = v3(0, 0, 0);
     int s = 0;
     PathState ps;
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, Ren
                 shade_now = true;
             } else {
                 if (fresh) {
-                    begin_sample(sc, a, sp, s, ps);
+                    begin_sample(sc, a, subpixel_of(a, id), s, ps);
                     fresh = false;
                 }
                 wr = ps.ray;
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, Ren
                 nverts += h.obj >= 0;
                 ShadowDefer df;
                 df.pending = false;
-                cont = shade_vertex<C>(sc, a, sp, s, ps, h, &df);
+                cont = shade_vertex<C>(sc, a, ps, h, &df);
                 phase = PH_TRACE;
                 if (df.pending) {
                     wr = Ray{df.o, df.d};
@@ -217,21 +218,16 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, Ren
         bool stop = false;
         if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
         long nid = wave_ticket(next_sub, done && !stop);
+        if (__any(done)) flush_count(a.counters, nverts);  // keeps the 32-bit lane counts far from overflow
         if (done) {
             id = stop ? nsub : nid;
             active = id < nsub;
-            if (active) sp = subpixel_of(a, id);
             acc = v3(0, 0, 0);
             s = 0;
             fresh = true;
         }
     }
-    if (a.counters) {
-        unsigned long long v = nverts;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        if (lane == 0 && v) atomicAdd(a.counters, v);
-    }
+    flush_count(a.counters, nverts);
 }
 
 // 4 subpixel means -> RGB8 (server.rs:360 clamp-then-average, :366-368 gamma, :187-189 `as u8`).
@@ -269,58 +265,67 @@ __global__ __launch_bounds__(256) void k_trace_f64(DevScene sc, long n, const do
     }
 }
 
+// Resident grid of a persistent kernel: as many 256-thread blocks as fit on the device at once.
+template <class K>
+static long resident_blocks(K kernel, long want) {
+    int dev = 0, ncu = 256, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    return std::max(1L, std::min((long)ncu * per_cu, want));
+}
+
+static int env_int(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    return v ? std::atoi(v) : dflt;
+}
+
+template <int F, int W>
+static void launch_mk(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
+                      hipStream_t st) {
+    const long blocks = resident_blocks(k_megakernel_f64<F, W>, (nsub + 255) / 256);
+    hipLaunchKernelGGL((k_megakernel_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub, nsub);
+}
+template <int F, int W>
+static void launch_mm(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
+                      int ksteps, hipStream_t st) {
+    const long blocks = resident_blocks(k_megakernel_mesh_f64<F, W>, (nsub + 255) / 256);
+    hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub,
+                       nsub, ksteps);
+}
+
 hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
                                  hipStream_t st) {
     const long nsub = (long)a.tw * a.th * 4;
     if (nsub <= 0 || a.n_samples <= 0) return hipSuccess;
-    // 4 waves/SIMD (128 VGPRs) measured fastest on every scene (profiles/r01_ab_waves.log);
-    // RT_MK_WAVES=1 selects the compiler's own allocation for A/B runs.
-    static const int waves = [] {
-        const char* v = std::getenv("RT_MK_WAVES");
-        return v ? std::atoi(v) : 4;
-    }();
-    int dev = 0, ncu = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const long resident = (long)ncu * (waves == 4 ? 4 : 2);  // 256-thread blocks per CU at that occupancy
-    const long blocks = std::max(1L, std::min(resident, (nsub + 255) / 256));
     hipError_t e = hipMemsetAsync(next_sub, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    dim3 g((unsigned)blocks), b(256);
-    // mesh scenes with compact tables and an octree of at least RT_MK_INTERLEAVE nodes: interleaved
-    // walks (0 selects the fused per-vertex traversal for A/B runs); RT_MK_KSTEPS walk steps per
-    // vertex iteration
-    static const int interleave = [] {
-        const char* v = std::getenv("RT_MK_INTERLEAVE");
-        return v ? std::atoi(v) : 64;
-    }();
-    static const int ksteps = [] {
-        const char* v = std::getenv("RT_MK_KSTEPS");
-        return v ? std::max(1, std::atoi(v)) : 8;
-    }();
-    static const int mwaves = [] {
-        const char* v = std::getenv("RT_MK_MESH_WAVES");
-        return v ? std::atoi(v) : 2;
-    }();
-    // shallow octrees (cubes: 9 nodes) walk in a few steps: the fused traversal is faster there
-    // (profiles/r01_interleave_ab.log)
+    // Occupancy (waves/SIMD requested from the register allocator): 4 (128 VGPRs, a few spills)
+    // measured fastest for the analytic scenes, 3 (no spills) for the fused mesh kernel
+    // (profiles/r01_waves_ab.log); RT_MK_WAVES=3|4 overrides for A/B runs.
+    static const int waves_env = env_int("RT_MK_WAVES", 0);
+    const int waves = waves_env ? waves_env : ((a.features & 1) ? 3 : 4);
+    // Mesh scenes with compact tables and an octree of at least RT_MK_INTERLEAVE nodes: interleaved
+    // walks, RT_MK_KSTEPS walk steps per vertex iteration, RT_MK_MESH_WAVES waves/SIMD (0 selects the
+    // fused per-vertex traversal for A/B runs). Shallow octrees (cubes: 9 nodes) walk in a few
+    // steps: the fused traversal is faster there (profiles/r01_interleave_ab.log).
+    static const int interleave = env_int("RT_MK_INTERLEAVE", 64);
+    static const int ksteps = std::max(1, env_int("RT_MK_KSTEPS", 8));
+    static const int mwaves = env_int("RT_MK_MESH_WAVES", 2);
     if (interleave && (a.features & 9) == 9 && a.mesh_nodes >= interleave) {
-        const long mres = (long)ncu * (mwaves == 4 ? 4 : 2);
-        const long mblocks = std::max(1L, std::min(mres, (nsub + 255) / 256));
-        dim3 mg((unsigned)mblocks);
-#define RT_MM_CASE(F)                                                                                                  \
-    case F:                                                                                                            \
-        if (mwaves == 4) hipLaunchKernelGGL((k_megakernel_mesh_f64<F, 4>), mg, b, 0, st, sc, a, sub_buf, next_sub, nsub, ksteps); \
-        else hipLaunchKernelGGL((k_megakernel_mesh_f64<F, 2>), mg, b, 0, st, sc, a, sub_buf, next_sub, nsub, ksteps);            \
+#define RT_MM_CASE(F)                                                                    \
+    case F:                                                                              \
+        if (mwaves == 4) launch_mm<F, 4>(sc, a, sub_buf, next_sub, nsub, ksteps, st);    \
+        else launch_mm<F, 2>(sc, a, sub_buf, next_sub, nsub, ksteps, st);                \
         break;
         switch (a.features & 15) { RT_MM_CASE(9) RT_MM_CASE(11) RT_MM_CASE(13) RT_MM_CASE(15) }
 #undef RT_MM_CASE
         return hipGetLastError();
     }
-#define RT_MK_CASE(F)                                                                                  \
-    case F:                                                                                            \
-        if (waves == 4) hipLaunchKernelGGL((k_megakernel_f64<F, 4>), g, b, 0, st, sc, a, sub_buf, next_sub, nsub); \
-        else hipLaunchKernelGGL((k_megakernel_f64<F, 1>), g, b, 0, st, sc, a, sub_buf, next_sub, nsub);            \
+#define RT_MK_CASE(F)                                                           \
+    case F:                                                                     \
+        if (waves == 3) launch_mk<F, 3>(sc, a, sub_buf, next_sub, nsub, st);    \
+        else launch_mk<F, 4>(sc, a, sub_buf, next_sub, nsub, st);               \
         break;
     switch (a.features & 15) {
         RT_MK_CASE(0) RT_MK_CASE(1) RT_MK_CASE(2) RT_MK_CASE(3) RT_MK_CASE(4) RT_MK_CASE(5) RT_MK_CASE(6)

@@ -339,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, 
             } else {
                 HitRec hr{ht[i], hobj[i], hprim[i]};
                 nverts += hr.obj >= 0;
-                emit = shade_vertex<C>(sc, a, sp, smp, ps, hr, kDefer ? &sd : nullptr);
+                emit = shade_vertex<C>(sc, a, ps, hr, kDefer ? &sd : nullptr);
                 finished = !emit;
                 if (finished && sd.pending) {
                     ps.kind = K_DONE;  // keep the path one more bounce for its shadow result
