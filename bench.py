@@ -2,9 +2,11 @@
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1 launched by
 torch.distributed.run, one rank per GPU. A step = one full render of the frame (scene resident in
-HBM; output RGB8 gathered to rank 0). The frame is split into N contiguous row stripes (image
-tiles; no collective on the data path except the final RGB8 gather the north_star prescribes),
-so total work is fixed: scaling = "strong". Rank 0 prints one JSON line.
+HBM; output RGB8 gathered to rank 0). Rank r renders the interleaved rows r, r+N, r+2N, ... of the
+frame (rt_render_params.row_step = N: every rank gets the same mix of cheap and expensive rows;
+--partition stripes gives contiguous stripes instead); no collective on the data path except the
+final RGB8 gather the north_star prescribes. Total work is fixed: scaling = "strong". Rank 0
+prints one JSON line.
 
 roofline: dominant kernel = the render kernel(s). Algorithmic bytes follow SURVEY §8(d)'s canonical
 SoA wavefront model, 88 B per camera sample + 280 B per path vertex, with the vertex count taken
@@ -46,6 +48,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=48)
     ap.add_argument("--cpu-spp", type=int, default=64)
+    ap.add_argument("--partition", choices=["interleave", "stripes"], default="interleave")
     return ap.parse_args()
 
 
@@ -53,6 +56,25 @@ def stripe(rank, world, height):
     y0 = rank * height // world
     y1 = (rank + 1) * height // world
     return y0, y1 - y0
+
+
+def partition(rank, world, height, mode="interleave"):
+    """Rows of rank `rank`: (y0, tile rows, row_step) — tile row i is screen row y0 + i * row_step."""
+    if mode == "stripes" or world == 1:
+        y0, th = stripe(rank, world, height)
+        return y0, th, 1
+    return rank, (height - rank + world - 1) // world, world
+
+
+def assemble(parts, world, height, mode="interleave"):
+    """Rank 0: puts the gathered row sets (each padded to the same row count) back into frame order."""
+    import numpy as np
+
+    frame = np.zeros((height,) + tuple(parts[0].shape[1:]), dtype=parts[0].dtype)
+    for r, p in enumerate(parts):
+        y0, th, step = partition(r, world, height, mode)
+        frame[y0:y0 + (th - 1) * step + 1:step] = p[:th]
+    return frame
 
 
 def cpu_baseline(args):
@@ -100,10 +122,11 @@ def main():
     import rt_amd
 
     scene = rt_amd.Scene.from_toml(os.path.join(REPO, "scenes", f"{args.scene}.toml"))
-    y0, th = stripe(rank, world, args.height)
+    y0, th, row_step = partition(rank, world, args.height, args.partition)
     flags = (rt_amd.FLAG_MEGAKERNEL if args.mode == "megakernel" else 0) | (rt_amd.FLAG_MIS if args.mis else 0)
-    params = rt_amd.make_params(args.width, args.height, args.spp, args.seed, (0, y0, args.width, th), flags, dev)
-    max_rows = (args.height + world - 1) // world
+    params = rt_amd.make_params(args.width, args.height, args.spp, args.seed, (0, y0, args.width, th), flags, dev,
+                                row_step)
+    max_rows = max(partition(r, world, args.height, args.partition)[1] for r in range(world))
     rgb = torch.zeros((max_rows, args.width, 3), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
     gathered = [torch.empty_like(rgb) for _ in range(world)] if (world > 1 and rank == 0) else None
@@ -143,6 +166,16 @@ def main():
     else:
         total_vertices = st["vertices"]
 
+    # the frame (rank 0): the gathered row sets put back in order; its digest is the same at every N
+    import hashlib
+
+    if rank == 0:
+        if world > 1:
+            frame = assemble([g.cpu().numpy() for g in gathered], world, args.height, args.partition)
+        else:
+            frame = rgb[:th].cpu().numpy()
+        digest = hashlib.sha1(frame.tobytes()).hexdigest()[:16]
+
     n_samples = args.width * args.height * 4 * (args.spp // 4)
     ms_per_step = wall * 1000.0 / args.steps
     value = n_samples / (wall / args.steps) / 1e6
@@ -170,7 +203,9 @@ def main():
                     f"{args.seed:#x}",
             "config": {"workload": workload, "scene": f"scenes/{args.scene}.toml", "width": args.width,
                        "height": args.height, "spp": args.spp, "traced_spp": 4 * (args.spp // 4),
-                       "mode": args.mode, "mis": args.mis, "parallelism": f"row stripes x{world}",
+                       "mode": args.mode, "mis": args.mis,
+                       "parallelism": f"{'interleaved rows' if args.partition == 'interleave' else 'row stripes'} x{world}",
+                       "frame_sha1": digest,
                        "vertices_per_sample": round(total_vertices / n_samples, 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

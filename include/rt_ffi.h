@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2  /* 2: rt_render_params.row_step */
 
 /* return codes */
 #define RT_OK 0
@@ -95,6 +95,8 @@ typedef struct {
     uint64_t seed;
     uint32_t flags;              /* RT_FLAG_* */
     int32_t device;              /* HIP device ordinal */
+    int32_t row_step;            /* tile row i is screen row y0 + i * row_step (0 or 1: contiguous rows);
+                                    k > 1 interleaves rows across k workers (multi-GPU load balance) */
 } rt_render_params;
 
 typedef struct {

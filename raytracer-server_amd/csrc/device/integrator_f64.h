@@ -43,7 +43,7 @@ RT_DEV SubPixel subpixel_of(const RenderArgs& a, long p) {
     SubPixel s;
     s.sub = (int)(p & 3);
     s.col = a.x0 + (int)(pix - r * tw);
-    int row = a.y0 + (int)r;
+    int row = a.y0 + (int)r * a.row_step;
     s.yref = a.height - row - 1;
     s.pid = (uint32_t)row * (uint32_t)a.width + (uint32_t)s.col;
     s.sx = s.sub & 1;

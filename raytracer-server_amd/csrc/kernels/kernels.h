@@ -14,6 +14,8 @@ struct RenderArgs {
     int32_t mis;
     int32_t features;  // Cfg<F> bits: 1 mesh, 2 phong, 4 mis (kernel specialisation)
     int32_t mesh_nodes;  // octree nodes of the largest mesh (megakernel choice)
+    int32_t row_step;    // tile row i = screen row y0 + i * row_step
+    int32_t pad1;
     uint64_t seed;
     double cx[3], cy[3];  // camera frame (server.rs:330-331), computed on the host
     double inv_n;         // 1.0 / n_samples (server.rs:358)

@@ -270,8 +270,10 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
 int check_params(const rt_render_params* p) {
     if (!p) return fail(RT_E_INVAL, "null params");
     if (p->width <= 0 || p->height <= 0) return fail(RT_E_INVAL, "width/height must be positive");
+    if (p->row_step < 0) return fail(RT_E_INVAL, "row_step must be >= 0");
+    const int64_t step = p->row_step > 1 ? p->row_step : 1;
     if (p->tile_w < 0 || p->tile_h < 0 || p->x0 < 0 || p->y0 < 0 || p->x0 + p->tile_w > p->width ||
-        p->y0 + p->tile_h > p->height)
+        (p->tile_h > 0 && p->y0 + (int64_t)(p->tile_h - 1) * step >= p->height))
         return fail(RT_E_INVAL, "tile outside the image");
     if ((int64_t)p->width * p->height > (int64_t)UINT32_MAX) return fail(RT_E_INVAL, "image too large for 32-bit pixel ids");
     return RT_OK;
@@ -309,6 +311,7 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
     a.height = p->height;
     a.x0 = p->x0;
     a.y0 = p->y0;
+    a.row_step = p->row_step > 1 ? p->row_step : 1;
     a.tw = p->tile_w;
     a.th = p->tile_h;
     a.n_samples = p->spp > 0 ? p->spp / 4 : 0;  // server.rs:332 (i32 division)

@@ -35,7 +35,7 @@ class RenderParams(ctypes.Structure):
     _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("x0", ctypes.c_int32),
                 ("y0", ctypes.c_int32), ("tile_w", ctypes.c_int32), ("tile_h", ctypes.c_int32),
                 ("spp", ctypes.c_int32), ("seed", ctypes.c_uint64), ("flags", ctypes.c_uint32),
-                ("device", ctypes.c_int32)]
+                ("device", ctypes.c_int32), ("row_step", ctypes.c_int32)]
 
 
 class RenderStats(ctypes.Structure):
@@ -227,16 +227,17 @@ class Scene:
         return t, ids, pos, nrm
 
 
-def make_params(width, height, spp, seed=0x5EED, tile=None, flags=0, device=0):
+def make_params(width, height, spp, seed=0x5EED, tile=None, flags=0, device=0, row_step=1):
+    """tile = (x0, y0, tile_w, tile_h); with row_step k > 1, tile row i is screen row y0 + i*k."""
     x0, y0, tw, th = tile if tile is not None else (0, 0, width, height)
-    return RenderParams(width, height, x0, y0, tw, th, spp, seed, flags, device)
+    return RenderParams(width, height, x0, y0, tw, th, spp, seed, flags, device, row_step)
 
 
 def render(scene, width, height, spp, seed=0x5EED, tile=None, mis=False, megakernel=False, device=0,
-           want_sub=False, cancel=None):
+           want_sub=False, cancel=None, row_step=1):
     """Renders a tile to host memory. Returns (rgb[th, tw, 3] u8, sub[th, tw, 4, 3] f64 or None, stats)."""
     flags = (FLAG_MIS if mis else 0) | (FLAG_MEGAKERNEL if megakernel else 0)
-    p = make_params(width, height, spp, seed, tile, flags, device)
+    p = make_params(width, height, spp, seed, tile, flags, device, row_step)
     rgb = np.zeros((p.tile_h, p.tile_w, 3), dtype=np.uint8)
     sub = np.zeros((p.tile_h, p.tile_w, 4, 3), dtype=np.float64) if want_sub else None
     st = RenderStats()

@@ -20,7 +20,7 @@ def test_exports_every_declared_symbol(rt):
     assert len(names) >= 11
     for n in names:
         assert hasattr(rt.lib, n), f"missing export {n}"
-    assert rt.lib.rt_abi_version() == 1
+    assert rt.lib.rt_abi_version() == 2
 
 
 def test_struct_layout_matches_header(rt, tmp_path):

@@ -100,6 +100,16 @@ def test_tiling_invariance_and_determinism(rt, gpu_scenes):
         t, sub_t, _ = rt.render(s, w, h, 8, SEED, tile=(x0, y0, tw, th), want_sub=True)
         assert np.array_equal(t, full[y0:y0 + th, x0:x0 + tw])
         assert np.array_equal(sub_t, sub_full[y0:y0 + th, x0:x0 + tw])
+    # interleaved rows (bench.py's multi-GPU partition): tile row i = screen row y0 + i * row_step
+    for mk in (True, False):
+        for (y0, step, x0, tw) in [(0, 3, 0, 200), (2, 3, 0, 200), (1, 7, 50, 100)]:
+            th = (h - y0 + step - 1) // step
+            t, sub_t, _ = rt.render(s, w, h, 8, SEED, tile=(x0, y0, tw, th), want_sub=True, row_step=step,
+                                    megakernel=mk)
+            assert np.array_equal(t, full[y0::step, x0:x0 + tw])
+            assert np.array_equal(sub_t, sub_full[y0::step, x0:x0 + tw])
+    with pytest.raises(rt.RtError):  # last row outside the image
+        rt.render(s, w, h, 8, SEED, tile=(0, 2, w, 50 + 1), row_step=3)
 
 
 def test_spp_semantics(rt, gpu_scenes, oracle_scenes):
