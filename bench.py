@@ -46,8 +46,8 @@ def parse():
     ap.add_argument("--mode", choices=["megakernel", "wavefront"], default=os.environ.get("RT_BENCH_MODE", "megakernel"))
     ap.add_argument("--mis", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=48)
-    ap.add_argument("--cpu-spp", type=int, default=64)
+    ap.add_argument("--cpu-rows", type=int, default=120)
+    ap.add_argument("--cpu-spp", type=int, default=256)
     ap.add_argument("--partition", choices=["interleave", "stripes"], default="interleave")
     return ap.parse_args()
 
