@@ -1,0 +1,19 @@
+/*
+ * rt_diag.h — diagnostics exported by librtamd.so next to the C ABI of rt_ffi.h (not part of the
+ * drop-in surface; used by tests and tools/).
+ */
+#ifndef RT_DIAG_H
+#define RT_DIAG_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* Device self-test of the exact-arithmetic shortcuts (path_f64.h: rcp_rn, qdiv) against IEEE
+ * division on n pseudo-random operands on the current HIP device; out[0] = reciprocal mismatches,
+ * out[1] = quotient mismatches. Returns 0 or -1 (HIP error). */
+int rt_selftest_arith(long n, unsigned long long seed, unsigned long long out[2]);
+/* RT_DEBUG_COUNTERS builds: octree traversal counters since the last call (zeros otherwise). */
+int rt_debug_counters(unsigned long long out[8]);
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_DIAG_H */

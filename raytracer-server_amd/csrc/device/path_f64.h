@@ -37,6 +37,19 @@ RT_DEV V3 operator*(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
 // [2^-900, 2^900]; otherwise, and for NaN/inf, the plain IEEE division is taken. r == 0 means q0
 // is the exact quotient (keeps the sign of a zero quotient). Bit-identical to a / b.
 RT_DEV bool rcp_safe(double b) { return fabs(b) >= 0x1p-900 && fabs(b) <= 0x1p900; }
+// RN(1 / b) for rcp_safe(b): the compiler's own IEEE f64 division sequence for 1.0 / b (v_rcp_f64,
+// two Newton steps, residual correction) without its range scaling (v_div_scale) and special-case
+// fixup (v_div_fixup), both identities in that range (every intermediate stays normal). 7 VALU
+// instead of 11; bit-identical to 1.0 / b (rt_selftest_arith, tests/test_gpu_parity.py).
+RT_DEV double rcp_rn(double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    double e = fma(-b, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-b, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-b, r, 1.0);
+    return fma(e, r, r);
+}
 RT_DEV double qdiv(double a, double b, double y) {
     double q0 = a * y;
     double r = fma(-b, q0, a);
@@ -44,7 +57,7 @@ RT_DEV double qdiv(double a, double b, double y) {
 }
 RT_DEV V3 operator/(V3 a, double s) {
     if (__all(rcp_safe(s))) {  // wave-uniform: no per-lane exec juggling on the common path
-        double y = 1.0 / s;
+        double y = rcp_rn(s);
         return v3(qdiv(a.x, s, y), qdiv(a.y, s, y), qdiv(a.z, s, y));
     }
     return v3(a.x / s, a.y / s, a.z / s);
@@ -125,9 +138,15 @@ struct RayInv {
 };
 RT_DEV RayInv make_inv(const V3& d) {
     RayInv v;
-    v.rx = 1.0 / d.x;
-    v.ry = 1.0 / d.y;
-    v.rz = 1.0 / d.z;
+    if (__all(rcp_safe(d.x) && rcp_safe(d.y) && rcp_safe(d.z))) {  // wave-uniform fast path
+        v.rx = rcp_rn(d.x);
+        v.ry = rcp_rn(d.y);
+        v.rz = rcp_rn(d.z);
+    } else {
+        v.rx = 1.0 / d.x;
+        v.ry = 1.0 / d.y;
+        v.rz = 1.0 / d.z;
+    }
     return v;
 }
 RT_DEV double div_x(double a, const Ray& r, const RayInv& v) { return qdiv(a, r.d.x, v.rx); }
@@ -216,7 +235,7 @@ RT_DEV bool tri_t(const DevTri& tr, const Ray& ray, double* tout) {
     double tn = det3(b, ab, ac), un = det3(nd, b, ac), vn = det3(nd, ab, b);
     double t, u, v;
     if (__all(rcp_safe(det))) {  // wave-uniform
-        double y = 1.0 / det;
+        double y = rcp_rn(det);
         t = qdiv(tn, det, y);
         u = qdiv(un, det, y);
         v = qdiv(vn, det, y);
@@ -863,7 +882,7 @@ RT_DEV void light_sample(const DevScene& sc, Rng& rng, V3* y, V3* ny, double* pd
         V3 n = norm(v3(x, yy, z));
         *y = ld3(L.pos) + n * L.r;
         *ny = n;
-        *pdf = 1.0 / (4.0 * PI * L.r * L.r);
+        *pdf = sc.light_pdf;  // 1.0 / (4.0 * PI * L.r * L.r), same bits (host, rt_api.cpp: upload)
         return;
     }
     // mesh light: area-weighted pick + Triangle::sample with the reference's missing `+ a`
@@ -883,11 +902,7 @@ RT_DEV void light_sample(const DevScene& sc, Rng& rng, V3* y, V3* ny, double* pd
     *ny = ld3(t.n);
     *pdf = 1. / m.surface_area;
 }
-RT_DEV double light_pdf_area(const DevScene& sc) {
-    const DevObject& L = sc.objects[sc.light];
-    if (L.geom == GEOM_SPHERE) return 1.0 / (4.0 * PI * L.r * L.r);
-    return 1. / sc.meshes[L.mesh].surface_area;
-}
+RT_DEV double light_pdf_area(const DevScene& sc) { return sc.light_pdf; }
 
 // Camera ray of server.rs:339-357 for subpixel (sx, sy) of pixel (x, y_ref).
 RT_DEV Ray camera_ray(const DevScene& sc, V3 cx, V3 cy, double w, double h, int x, int y, int sx, int sy, double u1,

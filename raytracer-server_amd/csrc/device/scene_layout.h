@@ -94,6 +94,8 @@ struct DevScene {
     const CompactTab* ctab;     // compact tables (valid when `compact`; see Cfg::compact)
     int32_t n_objects, light, n_meshes, compact;
     double cam_pos[3], cam_dir[3];
+    double light_pdf;           // area pdf of the light: 1 / (4 pi r^2) (geometry.rs:583) or
+                                // 1 / surface_area (:591), evaluated once on the host
 };
 
 }  // namespace rt

@@ -344,6 +344,43 @@ hipError_t launch_finalize_f64(const RenderArgs& a, const double* sub_buf, hipSt
     return hipGetLastError();
 }
 
+// Self-test of the exact-arithmetic shortcuts against the IEEE operations they replace: for n
+// pseudo-random (a, b) with |b| spread over [2^-900, 2^900] (every exponent, random and extreme
+// mantissas), counts rcp_rn(b) != 1.0 / b and qdiv(a, b, rcp_rn(b)) != a / b.
+__global__ void k_selftest_arith(long n, uint64_t seed, unsigned long long* bad) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Rng g(seed, (uint32_t)i, (uint32_t)(i >> 32), 7u);
+    const uint64_t m = g.next(), m2 = g.next(), sel = g.next();
+    uint64_t mant = m & 0xFFFFFFFFFFFFFull;
+    if ((sel & 7) == 0) mant = 0;                              // powers of two
+    if ((sel & 7) == 1) mant = 0xFFFFFFFFFFFFFull;             // just below
+    if ((sel & 7) == 2) mant = (sel >> 8) & 0xFF;              // just above
+    const int ex = -900 + (int)((sel >> 16) % 1801);
+    const uint64_t bits = ((uint64_t)(ex + 1023) << 52) | mant | ((sel >> 40) & 1 ? 0x8000000000000000ull : 0);
+    const double b = __longlong_as_double((long long)bits);
+    const double a = __longlong_as_double((long long)((m2 & 0x800FFFFFFFFFFFFFull) | ((uint64_t)(1023 + (int)((sel >> 48) % 200) - 100) << 52)));
+    const double y = rcp_rn(b);
+    unsigned long long e = 0;
+    if (__double_as_longlong(y) != __double_as_longlong(1.0 / b)) e |= 1;
+    if (__double_as_longlong(qdiv(a, b, y)) != __double_as_longlong(a / b)) e |= 2;
+    if (e & 1) atomicAdd(&bad[0], 1ull);
+    if (e & 2) atomicAdd(&bad[1], 1ull);
+}
+
+extern "C" int rt_selftest_arith(long n, unsigned long long seed, unsigned long long out[2]) {
+    unsigned long long* d = nullptr;
+    if (n <= 0 || hipMalloc(&d, 2 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    int rc = 0;
+    if (hipMemset(d, 0, 2 * sizeof(unsigned long long)) != hipSuccess) rc = -1;
+    if (!rc) {
+        hipLaunchKernelGGL(k_selftest_arith, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, n, seed, d);
+        if (hipGetLastError() != hipSuccess || hipMemcpy(out, d, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
+    }
+    (void)hipFree(d);
+    return rc;
+}
+
 // Diagnostic builds: read and clear the traversal counters (all zeros otherwise).
 extern "C" int rt_debug_counters(unsigned long long out[8]) {
 #if RT_DEBUG_COUNTERS

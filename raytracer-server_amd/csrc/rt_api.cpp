@@ -182,6 +182,13 @@ void fill_compact(const Packed& p, rt::CompactTab* ds, int32_t* compact) {
     for (size_t i = 0; i < p.objects.size(); ++i) {
         const rt::DevObject& o = p.objects[i];
         if (o.geom == rt::GEOM_PLANE && o.axis >= 0) {
+            // A later axis plane at the same coordinate as an earlier one yields the same t for
+            // every ray (the axis path divides (pos_k - o_k) by d_k only), so it can never be the
+            // nearest hit (ties go to the lower index, scene.rs:278) nor change a shadow test:
+            // leave it out (cornell_box.toml's "wall behind camera" repeats the right wall).
+            bool dup = false;
+            for (int j = 0; j < nax[o.axis]; ++j) dup |= ds->ax_pos[o.axis][j] == o.pos[o.axis];
+            if (dup) continue;
             if (nax[o.axis] == rt::kMaxAxisPlanes) { ok = false; break; }
             ds->ax_idx[o.axis][nax[o.axis]] = (int32_t)i;
             ds->ax_pos[o.axis][nax[o.axis]] = o.pos[o.axis];
@@ -256,6 +263,13 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.ctab = (const rt::CompactTab*)(b + o_tab);
         ds.compact = compact;
         ds.light = s->host.light;
+        ds.light_pdf = 0.0;
+        if (ds.light >= 0 && ds.light < (int32_t)p.objects.size()) {
+            const rt::DevObject& L = p.objects[ds.light];
+            const double PI = 3.14159265358979323846264338327950288;  // path_f64.h PI
+            if (L.geom == rt::GEOM_SPHERE) ds.light_pdf = 1.0 / (4.0 * PI * L.r * L.r);  // geometry.rs:583
+            else if (L.geom == rt::GEOM_MESH) ds.light_pdf = 1. / p.meshes[L.mesh].surface_area;  // :591
+        }
         ds.n_meshes = (int32_t)p.meshes.size();
         cp3(ds.cam_pos, s->host.cam_pos);
         cp3(ds.cam_dir, s->host.cam_dir);

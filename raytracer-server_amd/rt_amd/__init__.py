@@ -96,6 +96,11 @@ def _load():
     L.rt_last_error.argtypes = []
     L.rt_abi_version.argtypes = []
     L.rt_device_count.argtypes = []
+    # diagnostics (include/rt_diag.h)
+    if hasattr(L, "rt_selftest_arith"):  # absent from libraries built before it existed (A/B variants)
+        L.rt_selftest_arith.argtypes = [ctypes.c_long, ctypes.c_ulonglong, P(ctypes.c_ulonglong)]
+    if hasattr(L, "rt_debug_counters"):
+        L.rt_debug_counters.argtypes = [P(ctypes.c_ulonglong)]
     return L
 
 
@@ -298,6 +303,13 @@ class RenderJob:
         if st["cancelled"]:
             return []
         return list(chunk_messages(rgb))
+
+
+def selftest_arith(n=1 << 24, seed=0x5EED):
+    """Device check of the exact-division shortcuts: (reciprocal mismatches, quotient mismatches)."""
+    out = (ctypes.c_ulonglong * 2)()
+    _check(lib.rt_selftest_arith(n, seed, out))
+    return int(out[0]), int(out[1])
 
 
 def device_count():

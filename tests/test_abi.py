@@ -23,6 +23,14 @@ def test_exports_every_declared_symbol(rt):
     assert rt.lib.rt_abi_version() == 2
 
 
+def test_exports_diagnostics(rt):
+    text = open(os.path.join(REPO, "include", "rt_diag.h")).read()
+    names = re.findall(r"^int\s+(rt_[a-z_0-9]+)\s*\(", text, re.M)
+    assert names == ["rt_selftest_arith", "rt_debug_counters"]
+    for n in names:
+        assert hasattr(rt.lib, n), f"missing export {n}"
+
+
 def test_struct_layout_matches_header(rt, tmp_path):
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "rt_ffi.h"\nint main(void){'

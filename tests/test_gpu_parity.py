@@ -36,6 +36,11 @@ def _rays_for(name, n, rng):
     return o, d
 
 
+def test_exact_division_shortcuts(rt):
+    """rcp_rn / qdiv (path_f64.h) against IEEE division on the device: 2^24 operand pairs."""
+    assert rt.selftest_arith(1 << 24) == (0, 0)
+
+
 @pytest.mark.parametrize("name", ["cornell_box", "cubes", "flying_unicorn"])
 def test_trace_ray_bit_exact(name, gpu_scenes, oracle_scenes):
     rng = np.random.default_rng(1234)
