@@ -11,8 +11,11 @@ extern "C" {
  * division on n pseudo-random operands on the current HIP device; out[0] = reciprocal mismatches,
  * out[1] = quotient mismatches. Returns 0 or -1 (HIP error). */
 int rt_selftest_arith(long n, unsigned long long seed, unsigned long long out[2]);
-/* RT_DEBUG_COUNTERS builds: octree traversal counters since the last call (zeros otherwise). */
-int rt_debug_counters(unsigned long long out[8]);
+/* RT_DEBUG_COUNTERS builds: octree traversal counters since the last call (zeros otherwise):
+ * [0] walks [1] past the cull [2] node visits [3] leaves opened [4] triangle tests [5] walk steps;
+ * interleaved mesh megakernel: [8] wave iterations [9] lanes in the vertex phase [10] walk-loop
+ * wave steps [11] walking lanes summed over those steps. */
+int rt_debug_counters(unsigned long long out[16]);
 #ifdef __cplusplus
 }
 #endif

@@ -349,10 +349,14 @@ RT_DEV uint32_t octant_mask(const double* mn, const double* mx, const Ray& r, co
 
 // Diagnostic build only (make EXTRA=-DRT_DEBUG_COUNTERS=1): traversal work counters.
 #if RT_DEBUG_COUNTERS
-__device__ unsigned long long g_dbg[8];  // 0 walks, 1 past cull, 2 node visits, 3 leaves, 4 tri tests, 5 steps
+// 0 walks, 1 past cull, 2 node visits, 3 leaves, 4 tri tests, 5 steps; mesh megakernel (per wave):
+// 8 iterations, 9 lanes in the vertex phase, 10 walk-loop steps, 11 walking lanes over those steps
+__device__ unsigned long long g_dbg[16];
 #define RT_DBG(i) atomicAdd(&g_dbg[i], 1ull)
+#define RT_DBG_WAVE(i, pred) do { const unsigned long long m_ = __ballot(pred); if (__lane_id() == 0) atomicAdd(&g_dbg[i], (unsigned long long)__popcll(m_)); } while (0)
 #else
 #define RT_DBG(i) ((void)0)
+#define RT_DBG_WAVE(i, pred) ((void)0)
 #endif
 
 // Octree::intersect (geometry.rs:1237-1295) as a resumable per-lane walk.
@@ -368,31 +372,27 @@ __device__ unsigned long long g_dbg[8];  // 0 walks, 1 past cull, 2 node visits,
 // different lengths and refill lanes whose walk ended (persistent traversal kernels).
 struct OctWalk {
     double mn[3], mx[3];  // box of `cur`
-    int32_t kid[8];       // child table of `cur`
     int32_t cur, depth;
     uint32_t path;        // octant slot taken at each level, 3 bits per level (max depth 10)
     uint32_t pm;          // children of `cur` still to visit, bit q = visiting rank q
     uint64_t stk;         // pm of the ancestors at levels 0..7, 8 bits each
     uint32_t stk8;        // level 8 (parents exist at depths 0..9; MAX_DEPTH = 10)
-    uint32_t order, rank; // nibble q = octant visited q-th; nibble i = rank of octant i
+    uint32_t order;       // nibble q = octant visited q-th
     int32_t lpos, lend;   // leaf triangle cursor
     int32_t best;         // nearest triangle so far in the current leaf (ltri index), -1 none
     double bt;
 };
 
-RT_DEV void walk_load_kids(const DevScene& sc, OctWalk& w) {
-    const int4* k4 = reinterpret_cast<const int4*>(sc.node_kids + 8 * (size_t)w.cur);
-    const int4 a = k4[0], b = k4[1];
-    w.kid[0] = a.x; w.kid[1] = a.y; w.kid[2] = a.z; w.kid[3] = a.w;
-    w.kid[4] = b.x; w.kid[5] = b.y; w.kid[6] = b.z; w.kid[7] = b.w;
-}
-// Mask `cur`'s existing children whose boxes the ray hits, permuted to visiting order.
+// Mask `cur`'s existing children whose boxes the ray hits, permuted to visiting order. (The child
+// table itself is not kept in registers: a pick reads its one entry again, an L2 hit.)
 RT_DEV void walk_enter(const DevScene& sc, const Ray& ray, const RayInv& inv, OctWalk& w) {
     RT_DBG(2);
-    walk_load_kids(sc, w);
+    const int4* k4 = reinterpret_cast<const int4*>(sc.node_kids + 8 * (size_t)w.cur);
+    const int4 ka = k4[0], kb = k4[1];
+    const int32_t kid[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
     uint32_t m = octant_mask(w.mn, w.mx, ray, inv);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) m &= w.kid[i] == kKidEmpty ? ~(1u << i) : ~0u;
+    for (int i = 0; i < 8; ++i) m &= kid[i] == kKidEmpty ? ~(1u << i) : ~0u;
     uint32_t pm = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) pm |= ((m >> ((w.order >> (4 * q)) & 0xF)) & 1u) << q;
@@ -420,7 +420,6 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
         w.lpos = ls.x;
         w.lend = ls.x + ls.y;
         w.order = 0x76543210u;
-        w.rank = 0x76543210u;
         return true;
     }
     w.lpos = w.lend = 0;
@@ -445,11 +444,7 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
             }
         }
     }
-    uint32_t rank = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) rank |= (uint32_t)k << (4 * ((order >> (4 * k)) & 0xF));
     w.order = order;
-    w.rank = rank;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         w.mn[k] = m.root_box[k];
@@ -461,33 +456,53 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
 
 enum : int { WALK_RUN = 0, WALK_HIT = 1, WALK_MISS = 2 };
 
-// One unit of work. On WALK_HIT, *t / *prim hold the first hit subtree's nearest triangle.
+// One step of the walk. On WALK_HIT, *t / *prim hold the first hit subtree's nearest triangle.
+// A step tests up to kTrisPerStep triangles of the open leaf; when the leaf ends without a hit (or
+// no leaf is open) it pops every exhausted level at once, then picks the next child in visiting
+// order and either opens it (leaf) or descends into it and masks its children. Fewer, fuller steps
+// than one unit of work per step: a walk of the unicorn takes ~18 steps instead of ~39.
+#ifndef RT_TRIS_PER_STEP
+#define RT_TRIS_PER_STEP 2
+#endif
+constexpr int kTrisPerStep = RT_TRIS_PER_STEP;
 RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w, double* t,
                      int* prim) {
     RT_DBG(5);
-    if (w.lpos < w.lend) {  // one triangle of the open leaf
-        RT_DBG(4);
-        double tt;
-        if (tri_t(sc.ltris[w.lpos], ray, &tt) && (w.best < 0 || tt < w.bt)) {
-            w.bt = tt;
-            w.best = w.lpos;
+    if (w.lpos < w.lend) {  // triangles of the open leaf
+#pragma unroll
+        for (int j = 0; j < kTrisPerStep; ++j) {
+            if (w.lpos < w.lend) {
+                RT_DBG(4);
+                double tt;
+                if (tri_t(sc.ltris[w.lpos], ray, &tt) && (w.best < 0 || tt < w.bt)) {
+                    w.bt = tt;
+                    w.best = w.lpos;
+                }
+                ++w.lpos;
+            }
         }
-        if (++w.lpos < w.lend) return WALK_RUN;
+        if (w.lpos < w.lend) return WALK_RUN;
         if (w.best >= 0) {  // the first leaf with a hit wins (geometry.rs:1267-1269)
             *t = w.bt;
             *prim = sc.ltri_id[w.best];
             return WALK_HIT;
         }
-        return (w.depth == 0 && m.root_leaf >= 0) ? WALK_MISS : WALK_RUN;
     }
-    if (w.pm == 0) {  // `cur` exhausted: resume at its parent
-        if (w.depth == 0) return WALK_MISS;
-        w.cur = sc.node_up[w.cur].x;
-        const int lv = --w.depth;
-        w.pm = lv < 8 ? (uint32_t)(w.stk >> (8 * lv)) & 0xFFu : w.stk8;
+    if (w.pm == 0) {  // `cur` exhausted: resume at the nearest ancestor with children left
+        int lv = w.depth;
+        int32_t cur = w.cur;
+        uint32_t pm = 0;
+        while (pm == 0 && lv > 0) {
+            cur = sc.node_up[cur].x;
+            --lv;
+            pm = lv < 8 ? (uint32_t)(w.stk >> (8 * lv)) & 0xFFu : w.stk8;
+        }
+        if (pm == 0) return WALK_MISS;  // the root is exhausted
+        w.cur = cur;
+        w.depth = lv;
+        w.pm = pm;
         w.path &= (1u << (3 * lv)) - 1u;
-        walk_load_kids(sc, w);
-        // the parent's box, rebuilt from the root along the path (the build's own arithmetic)
+        // the ancestor's box, rebuilt from the root along the path (the build's own arithmetic)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             w.mn[k] = m.root_box[k];
@@ -501,14 +516,11 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
                 if ((oi >> (2 - k)) & 1u) w.mn[k] = c; else w.mx[k] = c;
             }
         }
-        return WALK_RUN;
     }
     const int q = __builtin_ctz(w.pm);
     w.pm &= w.pm - 1u;
     const uint32_t oi = (w.order >> (4 * q)) & 0xF;
-    int32_t c = w.kid[0];
-#pragma unroll
-    for (int j = 1; j < 8; ++j) c = oi == (uint32_t)j ? w.kid[j] : c;
+    const int32_t c = sc.node_kids[8 * (size_t)w.cur + oi];
     if (c <= -2) {  // open a leaf
         RT_DBG(3);
         const int2 ls = sc.leaf_span[-2 - c];

@@ -90,6 +90,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
     flush_count(a.counters, nverts);
 }
 
+__device__ __forceinline__ bool lane_id_is0() { return __lane_id() == 0; }
+
 // Begins the octree walk of the next candidate mesh after gen slot g (Scene::trace_ray's /
 // mutually_visible's loop over the mesh objects); false when no mesh is left.
 template <class C>
@@ -138,7 +140,10 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, Ren
     int g = -1, mi = 0;         // gen slot and mesh being walked
     OctWalk w;
     while (__any(active)) {
+        RT_DBG_WAVE(8, lane_id_is0());
         for (int k = 0; k < ksteps && __any(walking); ++k) {
+            RT_DBG_WAVE(10, lane_id_is0());
+            RT_DBG_WAVE(11, walking);
             if (walking) {
                 double t;
                 int prim;
@@ -157,6 +162,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, Ren
             }
         }
         bool done = false;
+        RT_DBG_WAVE(9, active && !walking);
         if (active && !walking) {
             bool shade_now = false, sample_end = false;
             if (phase == PH_WALK_SHADOW) {
@@ -382,13 +388,13 @@ extern "C" int rt_selftest_arith(long n, unsigned long long seed, unsigned long 
 }
 
 // Diagnostic builds: read and clear the traversal counters (all zeros otherwise).
-extern "C" int rt_debug_counters(unsigned long long out[8]) {
+extern "C" int rt_debug_counters(unsigned long long out[16]) {
 #if RT_DEBUG_COUNTERS
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(g_dbg)) != hipSuccess) return -1;
-    unsigned long long z[8] = {0};
+    unsigned long long z[16] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), z, sizeof(z)) != hipSuccess) return -1;
 #else
-    for (int i = 0; i < 8; ++i) out[i] = 0;
+    for (int i = 0; i < 16; ++i) out[i] = 0;
 #endif
     return 0;
 }
