@@ -585,6 +585,14 @@ RT_DEV bool object_t(const DevScene& sc, const DevObject& o, const Ray& ray, con
     return false;
 }
 
+// Geometry::intersect of a sphere or plane only (the analytic halves of the deferred queries: no
+// octree walk is compiled in, which the generic object_t would inline for a non-sphere/plane geom).
+RT_DEV bool analytic_t(const DevObject& o, const Ray& ray, const RayInv& inv, double* t) {
+    if (o.geom == GEOM_SPHERE) return sphere_t(o, ray, t);
+    if (o.geom == GEOM_PLANE) return plane_t(o, ray, inv, t);
+    return false;
+}
+
 struct HitRec {
     double t;
     int obj;   // -1: no hit
@@ -746,8 +754,7 @@ RT_DEV HitRec trace_analytic(const DevScene& sc, const Ray& ray, const RayInv& i
         const int idx = T->gen_idx[i];
         const DevObject& o = sc.objects[idx];
         double t;
-        int prim = -1;
-        if (o.geom != GEOM_MESH && object_t<C>(sc, o, ray, inv, &t, &prim)) consider(h, t, idx, prim);
+        if (analytic_t(o, ray, inv, &t)) consider(h, t, idx, -1);
     }
     return h;
 }
@@ -797,8 +804,7 @@ RT_DEV bool visible_analytic(const DevScene& sc, const Ray& r, const RayInv& inv
     for (int i = 0; i < T->n_gen; ++i) {
         const DevObject& o = sc.objects[T->gen_idx[i]];
         double t;
-        int prim;
-        if (o.geom != GEOM_MESH && object_t<C>(sc, o, r, inv, &t, &prim, dist) && !(t + ERR_MARGIN >= dist)) return false;
+        if (analytic_t(o, r, inv, &t) && !(t + ERR_MARGIN >= dist)) return false;
     }
     return true;
 }

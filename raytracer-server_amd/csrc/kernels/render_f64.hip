@@ -117,11 +117,72 @@ RT_DEV bool next_mesh_walk(const DevScene& sc, const Ray& r, const RayInv& inv, 
 // the reference's tie rule; shadow: the analytic objects let the ray through, then any mesh may
 // block it), so every path produces the same bits as k_megakernel_f64 (tested).
 enum : int { PH_TRACE = 0, PH_WALK_CLOSEST = 1, PH_WALK_SHADOW = 2 };
+
+// The walk state of each lane lives in LDS between walk phases ("parked"), one column per thread
+// of the block, so the vertex phase runs with the register footprint of the analytic kernel and
+// the walk phase holds only the path state plus the walk (no scratch spills at 2 waves/SIMD).
+// Doubles: ray o, d; 1/d; box mn, mx; walk best t; query t (closest hit so far / shadow distance);
+// pending NEE term. Ints: walk cursor fields, closest hit object/prim, gen slot, mesh, occluded.
+constexpr int kParkD = 21, kParkI = 16, kParkThreads = 256;
+typedef __attribute__((address_space(3))) double LdsDouble;
+typedef __attribute__((address_space(3))) int32_t LdsInt;
+struct Park {  // typed in the LDS address space: ds_read/ds_write with one 32-bit base + immediate offsets
+    LdsDouble* d;  // this thread's column of [kParkD][kParkThreads]
+    LdsInt* i;     // [kParkI][kParkThreads]
+    RT_DEV LdsDouble& D(int f) const { return d[f * kParkThreads]; }
+    RT_DEV LdsInt& I(int f) const { return i[f * kParkThreads]; }
+};
+struct WalkRegs {  // the walk phase's working copy
+    Ray wr;
+    RayInv wi;
+    OctWalk w;
+    double wt;  // closest: hit t so far (h.t); shadow: |y - x|
+    int32_t hobj, hprim, g, mi, occluded;
+};
+RT_DEV void park_store(const Park& p, const WalkRegs& r) {
+    p.D(0) = r.wr.o.x; p.D(1) = r.wr.o.y; p.D(2) = r.wr.o.z;
+    p.D(3) = r.wr.d.x; p.D(4) = r.wr.d.y; p.D(5) = r.wr.d.z;
+    p.D(6) = r.wi.rx; p.D(7) = r.wi.ry; p.D(8) = r.wi.rz;
+    for (int k = 0; k < 3; ++k) { p.D(9 + k) = r.w.mn[k]; p.D(12 + k) = r.w.mx[k]; }
+    p.D(15) = r.w.bt;
+    p.D(16) = r.wt;
+    p.I(0) = r.w.cur; p.I(1) = r.w.depth; p.I(2) = (int32_t)r.w.path; p.I(3) = (int32_t)r.w.pm;
+    p.I(4) = (int32_t)(uint32_t)r.w.stk; p.I(5) = (int32_t)(uint32_t)(r.w.stk >> 32); p.I(6) = (int32_t)r.w.stk8;
+    p.I(7) = (int32_t)r.w.order; p.I(8) = r.w.lpos; p.I(9) = r.w.lend; p.I(10) = r.w.best;
+    p.I(11) = r.hobj; p.I(12) = r.hprim; p.I(13) = r.g; p.I(14) = r.mi; p.I(15) = r.occluded;
+}
+RT_DEV void park_load(const Park& p, WalkRegs& r) {
+    r.wr.o = v3(p.D(0), p.D(1), p.D(2));
+    r.wr.d = v3(p.D(3), p.D(4), p.D(5));
+    r.wi.rx = p.D(6); r.wi.ry = p.D(7); r.wi.rz = p.D(8);
+    for (int k = 0; k < 3; ++k) { r.w.mn[k] = p.D(9 + k); r.w.mx[k] = p.D(12 + k); }
+    r.w.bt = p.D(15);
+    r.wt = p.D(16);
+    r.w.cur = p.I(0); r.w.depth = p.I(1); r.w.path = (uint32_t)p.I(2); r.w.pm = (uint32_t)p.I(3);
+    r.w.stk = (uint64_t)(uint32_t)p.I(4) | ((uint64_t)(uint32_t)p.I(5) << 32); r.w.stk8 = (uint32_t)p.I(6);
+    r.w.order = (uint32_t)p.I(7); r.w.lpos = p.I(8); r.w.lend = p.I(9); r.w.best = p.I(10);
+    r.hobj = p.I(11); r.hprim = p.I(12); r.g = p.I(13); r.mi = p.I(14); r.occluded = p.I(15);
+}
+
+// A new walk query: ray, 1/d, query t (closest analytic hit / shadow distance) and hit so far; the
+// first walk step begins the walk of the first candidate mesh (w.cur = -1: no walk in progress).
+RT_DEV void park_query(const Park& p, const Ray& r, const RayInv& wi, double wt, int32_t hobj, int32_t hprim) {
+    p.D(0) = r.o.x; p.D(1) = r.o.y; p.D(2) = r.o.z;
+    p.D(3) = r.d.x; p.D(4) = r.d.y; p.D(5) = r.d.z;
+    p.D(6) = wi.rx; p.D(7) = wi.ry; p.D(8) = wi.rz;
+    p.D(16) = wt;
+    p.I(0) = -1;
+    p.I(11) = hobj; p.I(12) = hprim; p.I(13) = -1; p.I(15) = 0;
+}
+
 template <int F, int W>
 __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
                                                                uint32_t* next_sub, long nsub, int ksteps) {
     using C = Cfg<F>;
     static_assert(C::mesh && C::compact, "mesh megakernel needs the compact tables");
+    __shared__ double s_park_d[kParkD * kParkThreads];
+    __shared__ int32_t s_park_i[kParkI * kParkThreads];
+    const Park park{(LdsDouble*)s_park_d + threadIdx.x, (LdsInt*)s_park_i + threadIdx.x};
     uint32_t nverts = 0;
     long id = wave_ticket(next_sub, true);
     bool active = id < nsub;
@@ -129,58 +190,73 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, Ren
     int s = 0;
     PathState ps;
     bool fresh = true;
-    // walk state: the walked ray (ps.ray for a closest query, the shadow ray for a shadow query)
     int phase = PH_TRACE;
-    bool walking = false, occluded = false, cont = false;
-    Ray wr;
-    RayInv wi;
-    double wdist = 0.0;         // shadow: |y - x|
-    HitRec h{0.0, -1, -1};      // closest: analytic hit merged with the finished mesh walks
-    V3 wc = v3(0, 0, 0);        // shadow: the pending NEE term (already weighted by beta)
-    int g = -1, mi = 0;         // gen slot and mesh being walked
-    OctWalk w;
+    bool walking = false, cont = false;
     while (__any(active)) {
         RT_DBG_WAVE(8, lane_id_is0());
-        for (int k = 0; k < ksteps && __any(walking); ++k) {
-            RT_DBG_WAVE(10, lane_id_is0());
-            RT_DBG_WAVE(11, walking);
-            if (walking) {
-                double t;
-                int prim;
-                const int st = walk_step(sc, sc.meshes[mi], wr, wi, w, &t, &prim);
-                if (st != WALK_RUN) {
-                    bool fin;
-                    if (phase == PH_WALK_CLOSEST) {
-                        if (st == WALK_HIT) consider(h, t, tables(sc)->gen_idx[g], prim);
-                        fin = !next_mesh_walk<C>(sc, wr, wi, h.obj >= 0 ? h.t : INFINITY, g, mi, w);
+        if (__any(walking)) {
+            WalkRegs r;
+            if (walking) park_load(park, r);
+            for (int k = 0; k < ksteps && __any(walking); ++k) {
+                RT_DBG_WAVE(10, lane_id_is0());
+                RT_DBG_WAVE(11, walking);
+                if (walking) {
+                    bool fin = false;
+                    if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
+                        const double tmax = phase == PH_WALK_CLOSEST ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
+                        fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w);
                     } else {
-                        occluded = st == WALK_HIT && !(t + 0.001 >= wdist);  // mutually_visible's ERR_MARGIN
-                        fin = occluded || !next_mesh_walk<C>(sc, wr, wi, wdist, g, mi, w);
+                        double t;
+                        int prim;
+                        const int st = walk_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim);
+                        if (st != WALK_RUN) {
+                            if (phase == PH_WALK_CLOSEST) {
+                                if (st == WALK_HIT) {
+                                    HitRec h{r.wt, r.hobj, r.hprim};
+                                    consider(h, t, tables(sc)->gen_idx[r.g], prim);
+                                    r.wt = h.t;
+                                    r.hobj = h.obj;
+                                    r.hprim = h.prim;
+                                }
+                            } else {
+                                r.occluded = st == WALK_HIT && !(t + 0.001 >= r.wt);  // mutually_visible's ERR_MARGIN
+                                fin = r.occluded;
+                            }
+                            r.w.cur = -1;  // next step: the next mesh, if any
+                        }
                     }
-                    walking = !fin;
+                    if (fin) {  // results for the vertex phase
+                        walking = false;
+                        park.D(16) = r.wt;
+                        park.I(11) = r.hobj;
+                        park.I(12) = r.hprim;
+                        park.I(15) = r.occluded;
+                    }
                 }
             }
+            if (walking) park_store(park, r);
         }
         bool done = false;
         RT_DBG_WAVE(9, active && !walking);
         if (active && !walking) {
             bool shade_now = false, sample_end = false;
+            HitRec h;
             if (phase == PH_WALK_SHADOW) {
-                if (!occluded) ps.L = ps.L + wc;
+                if (!park.I(15)) ps.L = ps.L + v3(park.D(17), park.D(18), park.D(19));
                 phase = PH_TRACE;
                 sample_end = !cont;
             } else if (phase == PH_WALK_CLOSEST) {
+                h = HitRec{park.D(16), park.I(11), park.I(12)};
                 shade_now = true;
             } else {
                 if (fresh) {
                     begin_sample(sc, a, subpixel_of(a, id), s, ps);
                     fresh = false;
                 }
-                wr = ps.ray;
-                wi = make_inv(wr.d);
-                h = trace_analytic<C>(sc, wr, wi);
-                g = -1;
-                if (next_mesh_walk<C>(sc, wr, wi, h.obj >= 0 ? h.t : INFINITY, g, mi, w)) {
+                const RayInv wi = make_inv(ps.ray.d);
+                h = trace_analytic<C>(sc, ps.ray, wi);
+                if (mesh_candidate<C>(sc, ps.ray, wi, h.obj >= 0 ? h.t : INFINITY)) {
+                    park_query(park, ps.ray, wi, h.t, h.obj, h.prim);
                     phase = PH_WALK_CLOSEST;
                     walking = true;
                 } else {
@@ -193,19 +269,14 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, Ren
                 df.pending = false;
                 cont = shade_vertex<C>(sc, a, ps, h, &df);
                 phase = PH_TRACE;
-                if (df.pending) {
-                    wr = Ray{df.o, df.d};
-                    wi = make_inv(wr.d);
-                    wdist = df.dist;
-                    wc = df.c;
-                    g = -1;
-                    occluded = false;
-                    if (next_mesh_walk<C>(sc, wr, wi, wdist, g, mi, w)) {
-                        phase = PH_WALK_SHADOW;
-                        walking = true;
-                    } else {
-                        ps.L = ps.L + wc;
-                    }
+                if (df.pending) {  // shade_vertex found a mesh that could block the shadow ray
+                    const Ray sr{df.o, df.d};
+                    park_query(park, sr, make_inv(sr.d), df.dist, -1, -1);
+                    park.D(17) = df.c.x;
+                    park.D(18) = df.c.y;
+                    park.D(19) = df.c.z;
+                    phase = PH_WALK_SHADOW;
+                    walking = true;
                 }
                 if (!walking) sample_end = !cont;
             }
@@ -312,17 +383,15 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double
     static const int waves_env = env_int("RT_MK_WAVES", 0);
     const int waves = waves_env ? waves_env : ((a.features & 1) ? 3 : 4);
     // Mesh scenes with compact tables and an octree of at least RT_MK_INTERLEAVE nodes: interleaved
-    // walks, RT_MK_KSTEPS walk steps per vertex iteration, RT_MK_MESH_WAVES waves/SIMD (0 selects the
-    // fused per-vertex traversal for A/B runs). Shallow octrees (cubes: 9 nodes) walk in a few
+    // walks, RT_MK_KSTEPS walk steps per vertex iteration, 2 waves/SIMD (the parked walk state takes
+    // 59 KB of LDS per block; 0 selects the fused per-vertex traversal for A/B runs). Shallow octrees (cubes: 9 nodes) walk in a few
     // steps: the fused traversal is faster there (profiles/r01_interleave_ab.log).
     static const int interleave = env_int("RT_MK_INTERLEAVE", 64);
     static const int ksteps = std::max(1, env_int("RT_MK_KSTEPS", 8));
-    static const int mwaves = env_int("RT_MK_MESH_WAVES", 2);
     if (interleave && (a.features & 9) == 9 && a.mesh_nodes >= interleave) {
-#define RT_MM_CASE(F)                                                                    \
-    case F:                                                                              \
-        if (mwaves == 4) launch_mm<F, 4>(sc, a, sub_buf, next_sub, nsub, ksteps, st);    \
-        else launch_mm<F, 2>(sc, a, sub_buf, next_sub, nsub, ksteps, st);                \
+#define RT_MM_CASE(F)                                                        \
+    case F:                                                                  \
+        launch_mm<F, 2>(sc, a, sub_buf, next_sub, nsub, ksteps, st);         \
         break;
         switch (a.features & 15) { RT_MM_CASE(9) RT_MM_CASE(11) RT_MM_CASE(13) RT_MM_CASE(15) }
 #undef RT_MM_CASE
