@@ -177,7 +177,7 @@ RT_DEV void park_query(const Park& p, const Ray& r, const RayInv& wi, double wt,
 
 template <int F, int W>
 __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
-                                                               uint32_t* next_sub, long nsub, int ksteps) {
+                                                               uint32_t* next_sub, long nsub, int ksteps, int wmin) {
     using C = Cfg<F>;
     static_assert(C::mesh && C::compact, "mesh megakernel needs the compact tables");
     __shared__ double s_park_d[kParkD * kParkThreads];
@@ -197,7 +197,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, Ren
         if (__any(walking)) {
             WalkRegs r;
             if (walking) park_load(park, r);
-            for (int k = 0; k < ksteps && __any(walking); ++k) {
+            // up to ksteps steps; after the first, only while at least wmin lanes still walk
+            for (int k = 0; k < ksteps && (k == 0 ? __any(walking) : __popcll(__ballot(walking)) >= wmin); ++k) {
                 RT_DBG_WAVE(10, lane_id_is0());
                 RT_DBG_WAVE(11, walking);
                 if (walking) {
@@ -365,10 +366,10 @@ static void launch_mk(const DevScene& sc, const RenderArgs& a, double* sub_buf, 
 }
 template <int F, int W>
 static void launch_mm(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
-                      int ksteps, hipStream_t st) {
+                      int ksteps, int wmin, hipStream_t st) {
     const long blocks = resident_blocks(k_megakernel_mesh_f64<F, W>, (nsub + 255) / 256);
     hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub,
-                       nsub, ksteps);
+                       nsub, ksteps, wmin);
 }
 
 hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
@@ -387,11 +388,12 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double
     // 59 KB of LDS per block; 0 selects the fused per-vertex traversal for A/B runs). Shallow octrees (cubes: 9 nodes) walk in a few
     // steps: the fused traversal is faster there (profiles/r01_interleave_ab.log).
     static const int interleave = env_int("RT_MK_INTERLEAVE", 64);
-    static const int ksteps = std::max(1, env_int("RT_MK_KSTEPS", 8));
+    static const int ksteps = std::max(1, env_int("RT_MK_KSTEPS", 4));
+    static const int wmin = std::max(1, env_int("RT_MK_WALK_MIN", 1));
     if (interleave && (a.features & 9) == 9 && a.mesh_nodes >= interleave) {
 #define RT_MM_CASE(F)                                                        \
     case F:                                                                  \
-        launch_mm<F, 2>(sc, a, sub_buf, next_sub, nsub, ksteps, st);         \
+        launch_mm<F, 2>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, st);   \
         break;
         switch (a.features & 15) { RT_MM_CASE(9) RT_MM_CASE(11) RT_MM_CASE(13) RT_MM_CASE(15) }
 #undef RT_MM_CASE
