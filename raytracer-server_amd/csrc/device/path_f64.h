@@ -296,13 +296,42 @@ RT_DEV bool near_box(const double* bx, const Ray& r, const RayInv& inv, double p
     return t0 <= t1 && t0 <= tmax * (1.0 + 1e-9) + 1e-9;
 }
 
-// shared by the traversal's child-order sort
-RT_DEV bool sqrt_gt(double a2, double b2) {
-    // sqrt(a2) > sqrt(b2) after rounding, without the square roots unless the radicands are within
-    // a few ulps (sqrt is monotone; a relative gap > 2^-50 survives both roundings).
-    if (!(a2 > b2)) return false;
-    if (a2 > b2 * (1.0 + 0x1p-50)) return true;
-    return sqrt(a2) > sqrt(b2);
+
+// The reference's child visiting order (geometry.rs:1248-1260): the 8 root octants insertion-sorted
+// by mag(centre - origin), swapping only while strictly greater — a stable sort, i.e. a sort by
+// (key, octant index). Done as Batcher's 19-comparator network on (key, index) pairs held in
+// registers (the unrolled insertion sort indexed d2[] by runtime nibbles: select chains, ~1000
+// VALU). Keys: the radicands d2 (sqrt is monotone); two radicands within 2^-50 of each other may
+// round to the same sqrt, so if any neighbours of the sorted order are that close the sort is redone
+// on the exact keys sqrt(d2) (rare, wave-divergent). Returns nibble q = octant visited q-th.
+RT_DEV uint32_t root_order(const double d2[8]) {
+    constexpr int net[19][2] = {{0, 1}, {2, 3}, {4, 5}, {6, 7}, {0, 2}, {1, 3}, {4, 6}, {5, 7}, {1, 2}, {5, 6},
+                                {0, 4}, {3, 7}, {1, 5}, {2, 6}, {1, 4}, {3, 6}, {2, 4}, {3, 5}, {3, 4}};
+    double k[8];
+    int ix[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { k[i] = d2[i]; ix[i] = i; }
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int c = 0; c < 19; ++c) {
+            const int a = net[c][0], b = net[c][1];
+            const bool sw = k[a] > k[b] || (k[a] == k[b] && ix[a] > ix[b]);
+            const double ka = k[a], kb = k[b];
+            const int ia = ix[a], ib = ix[b];
+            k[a] = sw ? kb : ka; k[b] = sw ? ka : kb;
+            ix[a] = sw ? ib : ia; ix[b] = sw ? ia : ib;
+        }
+        bool close = false;
+#pragma unroll
+        for (int q = 0; q < 7; ++q) close |= !(k[q + 1] > k[q] * (1.0 + 0x1p-50));
+        if (pass == 1 || !close) break;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { k[i] = sqrt(d2[i]); ix[i] = i; }  // mag() itself
+    }
+    uint32_t order = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) order |= (uint32_t)ix[q] << (4 * q);
+    return order;
 }
 
 // BoundingBox::intersect(..).is_some() (geometry.rs:977-1036) for all 8 octants of the box
@@ -429,22 +458,7 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
         V3 dv = ld3(m.oct_center[i]) - ray.o;
         d2[i] = dv.x * dv.x + dv.y * dv.y + dv.z * dv.z;  // mag()'s radicand, same operation order
     }
-    uint32_t order = 0x76543210u;
-#pragma unroll
-    for (int i = 1; i < 8; ++i) {
-#pragma unroll
-        for (int j = i; j > 0; --j) {
-            // insertion sort step (swap while strictly greater, geometry.rs:1251-1260)
-            int a = (order >> (4 * (j - 1))) & 0xF, b = (order >> (4 * j)) & 0xF;
-            if (sqrt_gt(d2[a], d2[b])) {
-                order &= ~((0xFu << (4 * (j - 1))) | (0xFu << (4 * j)));
-                order |= ((uint32_t)b << (4 * (j - 1))) | ((uint32_t)a << (4 * j));
-            } else {
-                break;
-            }
-        }
-    }
-    w.order = order;
+    w.order = root_order(d2);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         w.mn[k] = m.root_box[k];

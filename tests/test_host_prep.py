@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import scene_path
+from conftest import REPO, scene_path
 
 
 @pytest.mark.parametrize("name", ["cornell_box", "cubes", "flying_unicorn"])
@@ -127,3 +127,41 @@ def test_scene_create_from_desc_matches_toml(rt):
 def test_bad_desc_rejected(rt):
     with pytest.raises(rt.RtError):
         rt.Scene.from_desc([0, 0, 0], [0, 0, -1], [dict(geom_kind=2, mesh=3, emitted=[1, 1, 1])], [])
+
+
+def test_root_order_sorting_network():
+    """path_f64.h: root_order's 19-comparator network on (key, index) equals the reference's stable
+    insertion sort (geometry.rs:1248-1260) — 0-1 principle over all binary keys plus random keys
+    with ties. The network is read from the device source."""
+    import itertools
+    import random
+    import re
+
+    src = open(os.path.join(REPO, "raytracer-server_amd", "csrc", "device", "path_f64.h")).read()
+    body = re.search(r"constexpr int net\[19\]\[2\] = \{(.*?)\};", src, re.S).group(1)
+    net = [tuple(map(int, p)) for p in re.findall(r"\{(\d+), (\d+)\}", body)]
+    assert len(net) == 19
+
+    def network(keys):
+        a = [(k, i) for i, k in enumerate(keys)]
+        for x, y in net:
+            if a[x] > a[y]:
+                a[x], a[y] = a[y], a[x]
+        return [i for _, i in a]
+
+    def insertion(keys):
+        order = list(range(8))
+        for i in range(1, 8):
+            for j in range(i, 0, -1):
+                if keys[order[j - 1]] > keys[order[j]]:
+                    order[j - 1], order[j] = order[j], order[j - 1]
+                else:
+                    break
+        return order
+
+    for bits in itertools.product([0, 1], repeat=8):
+        assert network(list(bits)) == insertion(list(bits))
+    rnd = random.Random(5)
+    for _ in range(20000):
+        keys = [rnd.choice([0.5, 1.0, 2.0, rnd.random()]) for _ in range(8)]
+        assert network(keys) == insertion(keys)
