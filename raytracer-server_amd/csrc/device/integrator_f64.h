@@ -51,6 +51,32 @@ RT_DEV SubPixel subpixel_of(const RenderArgs& a, long p) {
     return s;
 }
 
+// Camera ray of sample `smp` of subpixel `sp` (server.rs:338-357): its direction and the sample's
+// RNG stream after the two camera draws.
+struct CameraSample {
+    V3 d;
+    uint64_t r0, r1;
+};
+RT_DEV CameraSample camera_sample(const DevScene& sc, const RenderArgs& a, const SubPixel& sp, int smp) {
+    Rng rng(a.seed, sp.pid, (uint32_t)smp, (uint32_t)sp.sub);
+    double u1 = rng.uniform(), u2 = rng.uniform();
+    const Ray r = camera_ray(sc, ld3(a.cx), ld3(a.cy), (double)a.width, (double)a.height, sp.col, sp.yref, sp.sx, sp.sy,
+                             u1, u2);
+    return CameraSample{r.d, rng.s0, rng.s1};
+}
+// New camera path from a camera sample.
+RT_DEV void begin_path(const DevScene& sc, const CameraSample& cs, PathState& ps) {
+    ps.r0 = cs.r0;
+    ps.r1 = cs.r1;
+    ps.ray = Ray{ld3(sc.cam_pos), cs.d};
+    ps.beta = v3(1, 1, 1);
+    ps.L = v3(0, 0, 0);
+    ps.bemit = v3(0, 0, 0);
+    ps.o = v3(0, 0, 0);
+    ps.pdf_prev = 0.0;
+    ps.depth = 0;
+    ps.kind = K_CAMERA;
+}
 // New camera path for sample `smp` of subpixel `sp` (server.rs:338-357).
 RT_DEV void begin_sample(const DevScene& sc, const RenderArgs& a, const SubPixel& sp, int smp, PathState& ps) {
     Rng rng(a.seed, sp.pid, (uint32_t)smp, (uint32_t)sp.sub);

@@ -46,7 +46,7 @@ __device__ __forceinline__ void flush_count(unsigned long long* counter, uint32_
 // W = minimum waves per SIMD requested from the register allocator.
 template <int F, int W>
 __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
-                                                          uint32_t* next_sub, long nsub) {
+                                                          uint32_t* next_sub, long nsub, int refill) {
     using C = Cfg<F>;
     uint32_t nverts = 0;
     long id = wave_ticket(next_sub, true);
@@ -55,10 +55,19 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
     int s = 0;
     PathState ps;
     bool fresh = true;
+    // Camera-sample buffer: the next sample's camera ray + RNG state, computed ahead in a pass the
+    // whole wave runs once >= refill lanes need one (begin_sample for the ~7% of lanes whose path
+    // ended each iteration otherwise runs every iteration at that lane utilisation).
+    CameraSample nb;
+    bool nvalid = false;
     while (__any(active)) {
         bool done = false;
         if (active) {
-            if (fresh) begin_sample(sc, a, subpixel_of(a, id), s, ps);
+            if (fresh) {
+                if (nvalid) begin_path(sc, nb, ps);
+                else begin_sample(sc, a, subpixel_of(a, id), s, ps);
+                nvalid = false;
+            }
             HitRec hr = trace_closest<C>(sc, ps.ray);
             nverts += hr.obj >= 0;
             fresh = !shade_vertex<C>(sc, a, ps, hr);
@@ -73,6 +82,14 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
                 }
             }
         }
+        // refill pass: lanes with a path in progress and a next sample in the same subpixel
+        const bool need = active && !fresh && !nvalid && s + 1 < a.n_samples;
+        if (refill > 0 && __popcll(__ballot(need)) >= refill) {
+            if (need) {
+                nb = camera_sample(sc, a, subpixel_of(a, id), s + 1);
+                nvalid = true;
+            }
+        }
         // cancellation (RenderJob::stop, server.rs:201-203): checked when a lane would start a new
         // subpixel; a set flag stops handing out work, lanes finish the subpixel they hold
         bool stop = false;
@@ -85,6 +102,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
             acc = v3(0, 0, 0);
             s = 0;
             fresh = true;
+            nvalid = false;
         }
     }
     flush_count(a.counters, nverts);
@@ -360,9 +378,10 @@ static int env_int(const char* name, int dflt) {
 
 template <int F, int W>
 static void launch_mk(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
-                      hipStream_t st) {
+                      int refill, hipStream_t st) {
     const long blocks = resident_blocks(k_megakernel_f64<F, W>, (nsub + 255) / 256);
-    hipLaunchKernelGGL((k_megakernel_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub, nsub);
+    hipLaunchKernelGGL((k_megakernel_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub, nsub,
+                       refill);
 }
 template <int F, int W>
 static void launch_mm(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
@@ -389,6 +408,8 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double
     // steps: the fused traversal is faster there (profiles/r01_interleave_ab.log).
     static const int interleave = env_int("RT_MK_INTERLEAVE", 64);
     static const int ksteps = std::max(1, env_int("RT_MK_KSTEPS", 4));
+    // camera-sample buffer refill threshold (lanes per wave; 0 disables the buffer)
+    static const int refill = env_int("RT_MK_CAM_REFILL", 24);
     static const int wmin = std::max(1, env_int("RT_MK_WALK_MIN", 1));
     if (interleave && (a.features & 9) == 9 && a.mesh_nodes >= interleave) {
 #define RT_MM_CASE(F)                                                        \
@@ -401,8 +422,8 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double
     }
 #define RT_MK_CASE(F)                                                           \
     case F:                                                                     \
-        if (waves == 3) launch_mk<F, 3>(sc, a, sub_buf, next_sub, nsub, st);    \
-        else launch_mk<F, 4>(sc, a, sub_buf, next_sub, nsub, st);               \
+        if (waves == 3) launch_mk<F, 3>(sc, a, sub_buf, next_sub, nsub, refill, st);    \
+        else launch_mk<F, 4>(sc, a, sub_buf, next_sub, nsub, refill, st);               \
         break;
     switch (a.features & 15) {
         RT_MK_CASE(0) RT_MK_CASE(1) RT_MK_CASE(2) RT_MK_CASE(3) RT_MK_CASE(4) RT_MK_CASE(5) RT_MK_CASE(6)
