@@ -83,8 +83,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
             }
         }
         // refill pass: lanes with a path in progress and a next sample in the same subpixel
-        const bool need = active && !fresh && !nvalid && s + 1 < a.n_samples;
-        if (refill > 0 && __popcll(__ballot(need)) >= refill) {
+        // (analytic scenes only: in the fused mesh kernel the extra registers cost more than it saves)
+        const bool need = !C::mesh && active && !fresh && !nvalid && s + 1 < a.n_samples;
+        if (!C::mesh && refill > 0 && __popcll(__ballot(need)) >= refill) {
             if (need) {
                 nb = camera_sample(sc, a, subpixel_of(a, id), s + 1);
                 nvalid = true;
