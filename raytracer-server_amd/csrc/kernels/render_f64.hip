@@ -44,27 +44,37 @@ __device__ __forceinline__ void flush_count(unsigned long long* counter, uint32_
 // sub_buf (sequential sum in sample order, server.rs:338-358) and the lane takes the next
 // subpixel. Waves idle only in the frame's final tail, not per wave.
 // W = minimum waves per SIMD requested from the register allocator.
+typedef __attribute__((address_space(3))) double LdsDouble;
+typedef __attribute__((address_space(3))) int32_t LdsInt;
+typedef __attribute__((address_space(3))) uint64_t LdsU64;
+
 template <int F, int W>
 __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
                                                           uint32_t* next_sub, long nsub, int refill) {
     using C = Cfg<F>;
+    // Rarely touched per-lane state lives in LDS (one column per thread; VGPRs are the limit at 4
+    // waves/SIMD): the subpixel accumulator (once per sample) and the camera-sample buffer — the
+    // next sample's camera ray + RNG state, computed ahead in a pass the whole wave runs once
+    // >= refill lanes need one (begin_sample for the ~7% of lanes whose path ended each iteration
+    // otherwise runs every iteration at that lane utilisation).
+    __shared__ double s_acc[3 * 256], s_nbd[3 * 256];
+    __shared__ uint64_t s_nbr[2 * 256];
+    LdsDouble* acc_l = (LdsDouble*)s_acc + threadIdx.x;  // component k at [k * 256]
+    LdsDouble* nbd = (LdsDouble*)s_nbd + threadIdx.x;
+    LdsU64* nbr = (LdsU64*)s_nbr + threadIdx.x;
     uint32_t nverts = 0;
     long id = wave_ticket(next_sub, true);
     bool active = id < nsub;
-    V3 acc = v3(0, 0, 0);
+    acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
     int s = 0;
     PathState ps;
     bool fresh = true;
-    // Camera-sample buffer: the next sample's camera ray + RNG state, computed ahead in a pass the
-    // whole wave runs once >= refill lanes need one (begin_sample for the ~7% of lanes whose path
-    // ended each iteration otherwise runs every iteration at that lane utilisation).
-    CameraSample nb;
     bool nvalid = false;
     while (__any(active)) {
         bool done = false;
         if (active) {
             if (fresh) {
-                if (nvalid) begin_path(sc, nb, ps);
+                if (nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[256], nbd[512]), nbr[0], nbr[256]}, ps);
                 else begin_sample(sc, a, subpixel_of(a, id), s, ps);
                 nvalid = false;
             }
@@ -72,7 +82,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
             nverts += hr.obj >= 0;
             fresh = !shade_vertex<C>(sc, a, ps, hr);
             if (fresh) {
+                V3 acc = v3(acc_l[0], acc_l[256], acc_l[512]);
                 acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                acc_l[0] = acc.x; acc_l[256] = acc.y; acc_l[512] = acc.z;
                 if (++s == a.n_samples) {
                     double* o = sub_buf + (size_t)id * 3;
                     o[0] = acc.x;
@@ -87,7 +99,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
         const bool need = !C::mesh && active && !fresh && !nvalid && s + 1 < a.n_samples;
         if (!C::mesh && refill > 0 && __popcll(__ballot(need)) >= refill) {
             if (need) {
-                nb = camera_sample(sc, a, subpixel_of(a, id), s + 1);
+                const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), s + 1);
+                nbd[0] = nb.d.x; nbd[256] = nb.d.y; nbd[512] = nb.d.z;
+                nbr[0] = nb.r0; nbr[256] = nb.r1;
                 nvalid = true;
             }
         }
@@ -100,7 +114,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
         if (done) {
             id = stop ? nsub : nid;
             active = id < nsub;
-            acc = v3(0, 0, 0);
+            acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
             s = 0;
             fresh = true;
             nvalid = false;
@@ -143,8 +157,6 @@ enum : int { PH_TRACE = 0, PH_WALK_CLOSEST = 1, PH_WALK_SHADOW = 2 };
 // Doubles: ray o, d; 1/d; box mn, mx; walk best t; query t (closest hit so far / shadow distance);
 // pending NEE term. Ints: walk cursor fields, closest hit object/prim, gen slot, mesh, occluded.
 constexpr int kParkD = 21, kParkI = 16, kParkThreads = 256;
-typedef __attribute__((address_space(3))) double LdsDouble;
-typedef __attribute__((address_space(3))) int32_t LdsInt;
 struct Park {  // typed in the LDS address space: ds_read/ds_write with one 32-bit base + immediate offsets
     LdsDouble* d;  // this thread's column of [kParkD][kParkThreads]
     LdsInt* i;     // [kParkI][kParkThreads]
