@@ -95,9 +95,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
             }
         }
         // refill pass: lanes with a path in progress and a next sample in the same subpixel
-        // (analytic scenes only: in the fused mesh kernel the extra registers cost more than it saves)
-        const bool need = !C::mesh && active && !fresh && !nvalid && s + 1 < a.n_samples;
-        if (!C::mesh && refill > 0 && __popcll(__ballot(need)) >= refill) {
+        const bool need = active && !fresh && !nvalid && s + 1 < a.n_samples;
+        if (refill > 0 && __popcll(__ballot(need)) >= refill) {
             if (need) {
                 const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), s + 1);
                 nbd[0] = nb.d.x; nbd[256] = nb.d.y; nbd[512] = nb.d.z;
@@ -208,19 +207,27 @@ RT_DEV void park_query(const Park& p, const Ray& r, const RayInv& wi, double wt,
 
 template <int F, int W>
 __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
-                                                               uint32_t* next_sub, long nsub, int ksteps, int wmin) {
+                                                               uint32_t* next_sub, long nsub, int ksteps, int wmin,
+                                                               int refill) {
     using C = Cfg<F>;
     static_assert(C::mesh && C::compact, "mesh megakernel needs the compact tables");
     __shared__ double s_park_d[kParkD * kParkThreads];
     __shared__ int32_t s_park_i[kParkI * kParkThreads];
     const Park park{(LdsDouble*)s_park_d + threadIdx.x, (LdsInt*)s_park_i + threadIdx.x};
+    // subpixel accumulator and camera-sample buffer in LDS, as in k_megakernel_f64
+    __shared__ double s_acc[3 * 256], s_nbd[3 * 256];
+    __shared__ uint64_t s_nbr[2 * 256];
+    LdsDouble* acc_l = (LdsDouble*)s_acc + threadIdx.x;
+    LdsDouble* nbd = (LdsDouble*)s_nbd + threadIdx.x;
+    LdsU64* nbr = (LdsU64*)s_nbr + threadIdx.x;
     uint32_t nverts = 0;
     long id = wave_ticket(next_sub, true);
     bool active = id < nsub;
-    V3 acc = v3(0, 0, 0);
+    acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
     int s = 0;
     PathState ps;
     bool fresh = true;
+    bool nvalid = false;
     int phase = PH_TRACE;
     bool walking = false, cont = false;
     while (__any(active)) {
@@ -282,7 +289,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, Ren
                 shade_now = true;
             } else {
                 if (fresh) {
-                    begin_sample(sc, a, subpixel_of(a, id), s, ps);
+                    if (nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[256], nbd[512]), nbr[0], nbr[256]}, ps);
+                    else begin_sample(sc, a, subpixel_of(a, id), s, ps);
+                    nvalid = false;
                     fresh = false;
                 }
                 const RayInv wi = make_inv(ps.ray.d);
@@ -313,7 +322,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, Ren
                 if (!walking) sample_end = !cont;
             }
             if (sample_end) {
+                V3 acc = v3(acc_l[0], acc_l[256], acc_l[512]);
                 acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                acc_l[0] = acc.x; acc_l[256] = acc.y; acc_l[512] = acc.z;
                 fresh = true;
                 if (++s == a.n_samples) {
                     double* o = sub_buf + (size_t)id * 3;
@@ -324,6 +335,17 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, Ren
                 }
             }
         }
+        // camera-sample refill pass: lanes with a path in progress (walking or not) and a next sample
+        // in the same subpixel
+        const bool need = active && !fresh && !nvalid && s + 1 < a.n_samples;
+        if (refill > 0 && __popcll(__ballot(need)) >= refill) {
+            if (need) {
+                const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), s + 1);
+                nbd[0] = nb.d.x; nbd[256] = nb.d.y; nbd[512] = nb.d.z;
+                nbr[0] = nb.r0; nbr[256] = nb.r1;
+                nvalid = true;
+            }
+        }
         bool stop = false;
         if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
         long nid = wave_ticket(next_sub, done && !stop);
@@ -331,9 +353,10 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, Ren
         if (done) {
             id = stop ? nsub : nid;
             active = id < nsub;
-            acc = v3(0, 0, 0);
+            acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
             s = 0;
             fresh = true;
+            nvalid = false;
         }
     }
     flush_count(a.counters, nverts);
@@ -398,10 +421,10 @@ static void launch_mk(const DevScene& sc, const RenderArgs& a, double* sub_buf, 
 }
 template <int F, int W>
 static void launch_mm(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
-                      int ksteps, int wmin, hipStream_t st) {
+                      int ksteps, int wmin, int refill, hipStream_t st) {
     const long blocks = resident_blocks(k_megakernel_mesh_f64<F, W>, (nsub + 255) / 256);
     hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub,
-                       nsub, ksteps, wmin);
+                       nsub, ksteps, wmin, refill);
 }
 
 hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
@@ -427,7 +450,7 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double
     if (interleave && (a.features & 9) == 9 && a.mesh_nodes >= interleave) {
 #define RT_MM_CASE(F)                                                        \
     case F:                                                                  \
-        launch_mm<F, 2>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, st);   \
+        launch_mm<F, 2>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, st);   \
         break;
         switch (a.features & 15) { RT_MM_CASE(9) RT_MM_CASE(11) RT_MM_CASE(13) RT_MM_CASE(15) }
 #undef RT_MM_CASE
