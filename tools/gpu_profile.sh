@@ -7,6 +7,8 @@ TAG=${TAG:-r01}
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo pytest FAIL; tail -20 gpurun_out/pytest_gpu.log; exit 1; }
 echo "pytest: $(tail -1 gpurun_out/pytest_gpu.log)"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1 || { echo smoke FAIL; tail -20 gpurun_out/smoke_${TAG}.log; exit 1; }
+tail -1 gpurun_out/smoke_${TAG}.log
 timeout -k 10 400 python bench.py > gpurun_out/bench_${TAG}.log 2>&1 || { echo bench FAIL; tail -20 gpurun_out/bench_${TAG}.log; exit 1; }
 tail -1 gpurun_out/bench_${TAG}.log
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python bench.py --no-cpu-baseline > gpurun_out/prof_${TAG}.log 2>&1 || { echo prof FAIL; tail -20 gpurun_out/prof_${TAG}.log; exit 1; }
