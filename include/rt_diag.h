@@ -16,6 +16,11 @@ int rt_selftest_arith(long n, unsigned long long seed, unsigned long long out[2]
  * interleaved mesh megakernel: [8] wave iterations [9] lanes in the vertex phase [10] walk-loop
  * wave steps [11] walking lanes summed over those steps. */
 int rt_debug_counters(unsigned long long out[16]);
+/* RT_DEBUG_COUNTERS builds: lane utilisation per instrumented code region (RT_DBG_REGION) since
+ * the last call: out[2i] = wave entries into region i, out[2i+1] = active lanes summed over them
+ * (i < 16); RT_DEBUG_TIMERS builds: out[32 + i] = s_memtime ticks of the megakernel's waves in timed
+ * region i (RT_DBG_TSTART / RT_DBG_TEND), summed over waves. */
+int rt_debug_regions(unsigned long long out[64]);
 #ifdef __cplusplus
 }
 #endif

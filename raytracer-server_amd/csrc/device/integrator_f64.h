@@ -108,9 +108,12 @@ template <class C>
 RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
                          const HitRec& hr, ShadowDefer* defer = nullptr) {
     if (hr.obj < 0) return false;  // no hit: R = 0 (scene.rs:157, :175, :233)
+    RT_DBG_REGION(6);
     const DevObject& obj = sc.objects[hr.obj];
     V3 x, nrm;
+    RT_DBG_TSTART(t_sf);
     surface<C>(sc, ps.ray, hr, &x, &nrm);
+    RT_DBG_TEND(7, t_sf);
     if (ps.kind == K_CAMERA) {
         ps.L = ld3(obj.emitted);
     } else if (ps.kind == K_SPEC) {
@@ -127,6 +130,7 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
     const double p = ps.depth <= (uint32_t)MAX_BOUNCES ? 1.0 : SURVIVAL_PROBABILITY;
     Rng rng(ps.r0, ps.r1);
     if (obj.brdf == BRDF_SPECULAR) {
+        RT_DBG_REGION(7);
         const bool survive = rng.uniform() < p;  // scene.rs:173
         ps.r0 = rng.s0;
         ps.r1 = rng.s1;
@@ -141,15 +145,19 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
         ps.kind = K_SPEC;
         return true;
     }
+    RT_DBG_REGION(8);
     const bool use_mis = C::mis && obj.brdf == BRDF_DIFFUSE;
     // next-event estimation (scene.rs:217-229)
     V3 y, ny;
     double pdfA;
+    RT_DBG_TSTART(t_ls);
     light_sample<C>(sc, rng, &y, &ny, &pdfA);
+    RT_DBG_TEND(9, t_ls);
     V3 i = norm(y - x);
     double r_sqr = dot(y - x, y - x);
     V3 lef = mult(ld3(sc.objects[sc.light].emitted), brdf_eval<C>(obj, nrm, ps.o, i));
     if (!is_zero(lef)) {  // a zero Le*f makes the term exactly 0: skip the shadow ray
+        RT_DBG_REGION(9);
         double vis;
         if constexpr (C::mesh && C::compact) {
             if (defer) {
@@ -169,7 +177,9 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
                 vis = visible<C>(sc, x, y) ? 1. : 0.;
             }
         } else {
+            RT_DBG_TSTART(t_vi);
             vis = visible<C>(sc, x, y) ? 1. : 0.;
+            RT_DBG_TEND(10, t_vi);
         }
         V3 c;
         if (!use_mis) {
@@ -186,9 +196,12 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
     }
     // Russian roulette + BSDF continuation (scene.rs:231-240)
     if (!(rng.uniform() < p)) return false;
+    RT_DBG_REGION(10);
     V3 wi;
     double pdf;
+    RT_DBG_TSTART(t_bs);
     brdf_sample<C>(obj, nrm, ps.o, rng, &wi, &pdf);
+    RT_DBG_TEND(11, t_bs);
     ps.r0 = rng.s0;
     ps.r1 = rng.s1;
     V3 f = brdf_eval<C>(obj, nrm, ps.o, wi);

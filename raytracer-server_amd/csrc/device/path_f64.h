@@ -383,9 +383,29 @@ RT_DEV uint32_t octant_mask(const double* mn, const double* mx, const Ray& r, co
 __device__ unsigned long long g_dbg[16];
 #define RT_DBG(i) atomicAdd(&g_dbg[i], 1ull)
 #define RT_DBG_WAVE(i, pred) do { const unsigned long long m_ = __ballot(pred); if (__lane_id() == 0) atomicAdd(&g_dbg[i], (unsigned long long)__popcll(m_)); } while (0)
+// lane utilisation of code region i (< 16): [2i] wave entries, [2i+1] active lanes summed over them
+__device__ unsigned long long g_dbg_region[32];
+#define RT_DBG_REGION(i) do { const unsigned long long m_ = __ballot(1); if (__lane_id() == __ffsll((long long)m_) - 1) { atomicAdd(&g_dbg_region[2 * (i)], 1ull); atomicAdd(&g_dbg_region[2 * (i) + 1], (unsigned long long)__popcll(m_)); } } while (0)
 #else
+#define RT_DBG_REGION(i) ((void)0)
 #define RT_DBG(i) ((void)0)
 #define RT_DBG_WAVE(i, pred) ((void)0)
+#endif
+// Diagnostic build only (make EXTRA=-DRT_DEBUG_TIMERS=1): wave time per code region i (< 16) in
+// s_memtime ticks, summed per wave in LDS (no global atomics on the path) and flushed to
+// g_dbg_time at the kernel's end; blocks of 256 threads (4 waves).
+#if RT_DEBUG_TIMERS
+__device__ unsigned long long g_dbg_time[16];
+__shared__ unsigned long long s_dbg_time[4 * 16];
+#define RT_DBG_TINIT() do { if (threadIdx.x < 64) s_dbg_time[threadIdx.x] = 0; __syncthreads(); } while (0)
+#define RT_DBG_TSTART(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define RT_DBG_TEND(i, v) do { const uint64_t d_ = __builtin_amdgcn_s_memtime() - (v); const unsigned long long m_ = __ballot(1); if (__lane_id() == __ffsll((long long)m_) - 1) atomicAdd(&s_dbg_time[(threadIdx.x >> 6) * 16 + (i)], (unsigned long long)d_); } while (0)
+#define RT_DBG_TFLUSH() do { __syncthreads(); if (threadIdx.x < 64) atomicAdd(&g_dbg_time[threadIdx.x & 15], s_dbg_time[threadIdx.x]); } while (0)
+#else
+#define RT_DBG_TINIT() ((void)0)
+#define RT_DBG_TSTART(v) ((void)0)
+#define RT_DBG_TEND(i, v) ((void)0)
+#define RT_DBG_TFLUSH() ((void)0)
 #endif
 
 // Octree::intersect (geometry.rs:1237-1295) as a resumable per-lane walk.
@@ -624,6 +644,7 @@ RT_DEV bool sphere_c(P c, const Ray& ray, double* tout) {
     double b = dot(op, ray.d);
     double det = b * b - dot(op, op) + c[3];
     if (det < 0.) return false;
+    RT_DBG_REGION(11);
     det = sqrt(det);
     double t = b - det;
     if (t > 1e-4) { *tout = t; return true; }
@@ -651,19 +672,24 @@ RT_DEV void axis_planes(const DevScene& sc, CTab* T, const Ray& ray, const RayIn
 
 template <class C>
 RT_DEV HitRec trace_closest(const DevScene& sc, const Ray& ray) {
+    RT_DBG_REGION(12);
     CTab* T = tables(sc);
     HitRec h{0.0, -1, -1};
+    RT_DBG_TSTART(t_pl);
     const RayInv inv = make_inv(ray.d);
     if constexpr (C::compact) {
         auto visit = [&](double t, int idx, int prim) { consider(h, t, idx, prim); };
         axis_planes<0>(sc, T, ray, inv, visit);
         axis_planes<1>(sc, T, ray, inv, visit);
         axis_planes<2>(sc, T, ray, inv, visit);
+        RT_DBG_TEND(13, t_pl);
+        RT_DBG_TSTART(t_sp);
 #pragma unroll
         for (int i = 0; i < kMaxSpheres; ++i) {
             double t;
             if (i < T->n_sph && sphere_c(T->sph[i], ray, &t)) consider(h, t, T->sph_idx[i], -1);
         }
+        RT_DBG_TEND(14, t_sp);
         for (int i = 0; i < T->n_gen; ++i) {
             const int idx = T->gen_idx[i];
             double t;
@@ -713,6 +739,7 @@ template <class C>
 RT_DEV bool visible(const DevScene& sc, V3 x, V3 y) {
     CTab* T = tables(sc);
     const double ERR_MARGIN = 0.001;
+    RT_DBG_REGION(13);
     V3 diff = y - x;
     double dist = mag(diff);
     Ray r{x, diff / dist};  // norm(diff), sharing the magnitude

@@ -62,6 +62,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
     LdsDouble* acc_l = (LdsDouble*)s_acc + threadIdx.x;  // component k at [k * 256]
     LdsDouble* nbd = (LdsDouble*)s_nbd + threadIdx.x;
     LdsU64* nbr = (LdsU64*)s_nbr + threadIdx.x;
+    RT_DBG_TINIT();
     uint32_t nverts = 0;
     long id = wave_ticket(next_sub, true);
     bool active = id < nsub;
@@ -71,17 +72,29 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
     bool fresh = true;
     bool nvalid = false;
     while (__any(active)) {
+        RT_DBG_REGION(0);
+        RT_DBG_TSTART(t_it);
         bool done = false;
         if (active) {
+            RT_DBG_REGION(1);
+            RT_DBG_TSTART(t_fr);
             if (fresh) {
+                RT_DBG_REGION(2);
                 if (nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[256], nbd[512]), nbr[0], nbr[256]}, ps);
-                else begin_sample(sc, a, subpixel_of(a, id), s, ps);
+                else { RT_DBG_REGION(5); begin_sample(sc, a, subpixel_of(a, id), s, ps); }
                 nvalid = false;
             }
+            RT_DBG_TEND(1, t_fr);
+            RT_DBG_TSTART(t_tr);
             HitRec hr = trace_closest<C>(sc, ps.ray);
+            RT_DBG_TEND(2, t_tr);
             nverts += hr.obj >= 0;
+            RT_DBG_TSTART(t_sh);
             fresh = !shade_vertex<C>(sc, a, ps, hr);
+            RT_DBG_TEND(3, t_sh);
+            RT_DBG_TSTART(t_se);
             if (fresh) {
+                RT_DBG_REGION(4);
                 V3 acc = v3(acc_l[0], acc_l[256], acc_l[512]);
                 acc = acc + ps.L * a.inv_n;  // server.rs:357-358
                 acc_l[0] = acc.x; acc_l[256] = acc.y; acc_l[512] = acc.z;
@@ -93,17 +106,22 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
                     done = true;
                 }
             }
+            RT_DBG_TEND(6, t_se);
         }
+        RT_DBG_TSTART(t_rf);
         // refill pass: lanes with a path in progress and a next sample in the same subpixel
         const bool need = active && !fresh && !nvalid && s + 1 < a.n_samples;
         if (refill > 0 && __popcll(__ballot(need)) >= refill) {
             if (need) {
+                RT_DBG_REGION(3);
                 const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), s + 1);
                 nbd[0] = nb.d.x; nbd[256] = nb.d.y; nbd[512] = nb.d.z;
                 nbr[0] = nb.r0; nbr[256] = nb.r1;
                 nvalid = true;
             }
         }
+        RT_DBG_TEND(4, t_rf);
+        RT_DBG_TSTART(t_bk);
         // cancellation (RenderJob::stop, server.rs:201-203): checked when a lane would start a new
         // subpixel; a set flag stops handing out work, lanes finish the subpixel they hold
         bool stop = false;
@@ -118,8 +136,11 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
             fresh = true;
             nvalid = false;
         }
+        RT_DBG_TEND(5, t_bk);
+        RT_DBG_TEND(0, t_it);
     }
     flush_count(a.counters, nverts);
+    RT_DBG_TFLUSH();
 }
 
 __device__ __forceinline__ bool lane_id_is0() { return __lane_id() == 0; }
@@ -516,6 +537,21 @@ extern "C" int rt_selftest_arith(long n, unsigned long long seed, unsigned long 
 }
 
 // Diagnostic builds: read and clear the traversal counters (all zeros otherwise).
+extern "C" int rt_debug_regions(unsigned long long out[64]) {
+    for (int i = 0; i < 64; ++i) out[i] = 0;
+    unsigned long long z[32] = {0};
+#if RT_DEBUG_COUNTERS
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_region), sizeof(g_dbg_region)) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_region), z, sizeof(g_dbg_region)) != hipSuccess) return -1;
+#endif
+#if RT_DEBUG_TIMERS
+    if (hipMemcpyFromSymbol(out + 32, HIP_SYMBOL(g_dbg_time), sizeof(g_dbg_time)) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_time), z, sizeof(g_dbg_time)) != hipSuccess) return -1;
+#endif
+    (void)z;
+    return 0;
+}
+
 extern "C" int rt_debug_counters(unsigned long long out[16]) {
 #if RT_DEBUG_COUNTERS
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(g_dbg)) != hipSuccess) return -1;

@@ -101,6 +101,8 @@ def _load():
         L.rt_selftest_arith.argtypes = [ctypes.c_long, ctypes.c_ulonglong, P(ctypes.c_ulonglong)]
     if hasattr(L, "rt_debug_counters"):
         L.rt_debug_counters.argtypes = [P(ctypes.c_ulonglong)]
+    if hasattr(L, "rt_debug_regions"):
+        L.rt_debug_regions.argtypes = [P(ctypes.c_ulonglong)]
     return L
 
 

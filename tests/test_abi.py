@@ -26,7 +26,7 @@ def test_exports_every_declared_symbol(rt):
 def test_exports_diagnostics(rt):
     text = open(os.path.join(REPO, "include", "rt_diag.h")).read()
     names = re.findall(r"^int\s+(rt_[a-z_0-9]+)\s*\(", text, re.M)
-    assert names == ["rt_selftest_arith", "rt_debug_counters"]
+    assert names == ["rt_selftest_arith", "rt_debug_counters", "rt_debug_regions"]
     for n in names:
         assert hasattr(rt.lib, n), f"missing export {n}"
 
