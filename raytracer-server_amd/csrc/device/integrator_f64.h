@@ -17,6 +17,14 @@
 #include "../kernels/kernels.h"
 #include "path_f64.h"
 
+// A/B switches of the shading restructure (1 = on)
+#ifndef RT_OPT_SPEC
+#define RT_OPT_SPEC 1  // mirror vertices share the RR + continuation code of diffuse vertices
+#endif
+#ifndef RT_OPT_VIS
+#define RT_OPT_VIS 1   // the shadow ray reuses norm(y - x) and |y - x| of the NEE term
+#endif
+
 namespace rt {
 namespace f64 {
 
@@ -129,7 +137,9 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
     ps.depth += 1;
     const double p = ps.depth <= (uint32_t)MAX_BOUNCES ? 1.0 : SURVIVAL_PROBABILITY;
     Rng rng(ps.r0, ps.r1);
-    if (obj.brdf == BRDF_SPECULAR) {
+    const bool spec = obj.brdf == BRDF_SPECULAR;
+#if !RT_OPT_SPEC
+    if (spec) {
         RT_DBG_REGION(7);
         const bool survive = rng.uniform() < p;  // scene.rs:173
         ps.r0 = rng.s0;
@@ -145,56 +155,71 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
         ps.kind = K_SPEC;
         return true;
     }
-    RT_DBG_REGION(8);
+#endif
     const bool use_mis = C::mis && obj.brdf == BRDF_DIFFUSE;
-    // next-event estimation (scene.rs:217-229)
-    V3 y, ny;
-    double pdfA;
-    RT_DBG_TSTART(t_ls);
-    light_sample<C>(sc, rng, &y, &ny, &pdfA);
-    RT_DBG_TEND(9, t_ls);
-    V3 i = norm(y - x);
-    double r_sqr = dot(y - x, y - x);
-    V3 lef = mult(ld3(sc.objects[sc.light].emitted), brdf_eval<C>(obj, nrm, ps.o, i));
-    if (!is_zero(lef)) {  // a zero Le*f makes the term exactly 0: skip the shadow ray
-        RT_DBG_REGION(9);
-        double vis;
-        if constexpr (C::mesh && C::compact) {
-            if (defer) {
-                // mutually_visible (scene.rs:258-270) split: analytic objects now, meshes deferred
-                V3 diff = y - x;
-                double dist = mag(diff);
-                Ray sr{x, diff / dist};
-                const RayInv inv = make_inv(sr.d);
-                vis = visible_analytic<C>(sc, sr, inv, dist) ? 1. : 0.;
-                if (vis > 0. && mesh_candidate<C>(sc, sr, inv, dist)) {
-                    defer->pending = true;
-                    defer->o = sr.o;
-                    defer->d = sr.d;
-                    defer->dist = dist;
+    // next-event estimation (scene.rs:217-229); a mirror vertex has none (scene.rs:170-185)
+    if (!spec) {
+        RT_DBG_REGION(8);
+        V3 y, ny;
+        double pdfA;
+        RT_DBG_TSTART(t_ls);
+        light_sample<C>(sc, rng, &y, &ny, &pdfA);
+        RT_DBG_TEND(9, t_ls);
+        const V3 diff = y - x;
+        const double r_sqr = dot(diff, diff);
+#if RT_OPT_VIS
+        // norm(y - x) and |y - x| exactly as mutually_visible computes them (scene.rs:258-262): the
+        // shadow ray reuses them
+        const double dist = sqrt(r_sqr);  // == mag(diff)
+        const V3 i = diff / dist;          // == norm(diff)
+#else
+        const V3 i = norm(diff);
+#endif
+        V3 lef = mult(ld3(sc.objects[sc.light].emitted), brdf_eval<C>(obj, nrm, ps.o, i));
+        if (!is_zero(lef)) {  // a zero Le*f makes the term exactly 0: skip the shadow ray
+            RT_DBG_REGION(9);
+            double vis;
+#if RT_OPT_VIS
+            const Ray sr{x, i};
+#else
+            const double dist = mag(diff);
+            const Ray sr{x, diff / dist};
+#endif
+            if constexpr (C::mesh && C::compact) {
+                if (defer) {
+                    // mutually_visible (scene.rs:258-270) split: analytic objects now, meshes deferred
+                    const RayInv inv = make_inv(sr.d);
+                    vis = visible_analytic<C>(sc, sr, inv, dist) ? 1. : 0.;
+                    if (vis > 0. && mesh_candidate<C>(sc, sr, inv, dist)) {
+                        defer->pending = true;
+                        defer->o = sr.o;
+                        defer->d = sr.d;
+                        defer->dist = dist;
+                    }
+                } else {
+                    vis = visible_ray<C>(sc, sr, dist) ? 1. : 0.;
                 }
             } else {
-                vis = visible<C>(sc, x, y) ? 1. : 0.;
+                RT_DBG_TSTART(t_vi);
+                vis = visible_ray<C>(sc, sr, dist) ? 1. : 0.;
+                RT_DBG_TEND(10, t_vi);
             }
-        } else {
-            RT_DBG_TSTART(t_vi);
-            vis = visible<C>(sc, x, y) ? 1. : 0.;
-            RT_DBG_TEND(10, t_vi);
+            V3 c;
+            if (!use_mis) {
+                c = lef * vis * dot(nrm, i) * dot(ny, -i) / (r_sqr * pdfA);
+            } else {
+                double cosl = dot(ny, -i);
+                double pdf_l = pdfA * r_sqr / cosl;
+                double pdf_b = dot(nrm, i) * FRAC_1_PI;
+                c = v3(0, 0, 0);
+                if (vis > 0. && cosl > 0. && pdf_b > 0.) c = lef * dot(nrm, i) * ((pdf_l / (pdf_l + pdf_b)) / pdf_l);
+            }
+            if (defer && defer->pending) defer->c = mult(ps.beta, c);  // added later iff no mesh occludes
+            else ps.L = ps.L + mult(ps.beta, c);
         }
-        V3 c;
-        if (!use_mis) {
-            c = lef * vis * dot(nrm, i) * dot(ny, -i) / (r_sqr * pdfA);
-        } else {
-            double cosl = dot(ny, -i);
-            double pdf_l = pdfA * r_sqr / cosl;
-            double pdf_b = dot(nrm, i) * FRAC_1_PI;
-            c = v3(0, 0, 0);
-            if (vis > 0. && cosl > 0. && pdf_b > 0.) c = lef * dot(nrm, i) * ((pdf_l / (pdf_l + pdf_b)) / pdf_l);
-        }
-        if (defer && defer->pending) defer->c = mult(ps.beta, c);  // added later iff no mesh occludes
-        else ps.L = ps.L + mult(ps.beta, c);
     }
-    // Russian roulette + BSDF continuation (scene.rs:231-240)
+    // Russian roulette (scene.rs:173 / :231) + BSDF continuation (scene.rs:176-184 / :232-240): one
+    // code path for mirror and diffuse vertices
     if (!(rng.uniform() < p)) return false;
     RT_DBG_REGION(10);
     V3 wi;
@@ -205,13 +230,15 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
     ps.r0 = rng.s0;
     ps.r1 = rng.s1;
     V3 f = brdf_eval<C>(obj, nrm, ps.o, wi);
+    if (spec) ps.bemit = ps.beta;  // Le(x') after a mirror bounce is weighted by the beta before it
     ps.beta = mult(ps.beta, f) * dot(nrm, wi) / (pdf * p);
     ps.ray = Ray{x, wi};
-    ps.kind = K_DIFF;
+    ps.kind = spec ? K_SPEC : K_DIFF;
     ps.pdf_prev = use_mis ? pdf : 0.0;
-    // zero throughput: every later term is exactly 0, and with a counter-based RNG no draws need
-    // to be kept in step — end the path (same result, less work)
-    return !is_zero(ps.beta);
+    // zero throughput: every later term is exactly 0 (a mirror bounce's Le(x') still counts, with the
+    // beta before it), and with a counter-based RNG no draws need to be kept in step — end the path
+    // (same result, less work)
+    return spec || !is_zero(ps.beta);
 }
 
 }  // namespace f64

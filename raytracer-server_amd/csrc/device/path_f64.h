@@ -735,14 +735,13 @@ RT_DEV void surface(const DevScene& sc, const Ray& ray, const HitRec& h, V3* pos
 // Scene::mutually_visible (scene.rs:258-270) as an any-hit query: occluded iff some object's
 // intersect t satisfies t + 0.001 < |y - x| (equivalent to the nearest-hit test because x + 0.001
 // rounds monotonically). Analytic objects are tested before meshes (order-free for a boolean).
+// r = {x, norm(y - x)} and dist = mag(y - x) as the caller computed them (visible() below, or the
+// NEE term's own values: same bits).
 template <class C>
-RT_DEV bool visible(const DevScene& sc, V3 x, V3 y) {
+RT_DEV bool visible_ray(const DevScene& sc, const Ray& r, double dist) {
+    RT_DBG_REGION(13);
     CTab* T = tables(sc);
     const double ERR_MARGIN = 0.001;
-    RT_DBG_REGION(13);
-    V3 diff = y - x;
-    double dist = mag(diff);
-    Ray r{x, diff / dist};  // norm(diff), sharing the magnitude
     const RayInv inv = make_inv(r.d);
     if constexpr (C::compact) {
         bool occluded = false;
@@ -774,6 +773,12 @@ RT_DEV bool visible(const DevScene& sc, V3 x, V3 y) {
         }
     }
     return true;
+}
+template <class C>
+RT_DEV bool visible(const DevScene& sc, V3 x, V3 y) {
+    V3 diff = y - x;
+    double dist = mag(diff);
+    return visible_ray<C>(sc, Ray{x, diff / dist}, dist);  // norm(diff), sharing the magnitude
 }
 
 // ---- pieces of trace_ray / mutually_visible for the wavefront's deferred mesh queries ----

@@ -44,6 +44,9 @@ __device__ __forceinline__ void flush_count(unsigned long long* counter, uint32_
 // sub_buf (sequential sum in sample order, server.rs:338-358) and the lane takes the next
 // subpixel. Waves idle only in the frame's final tail, not per wave.
 // W = minimum waves per SIMD requested from the register allocator.
+#ifndef RT_OPT_CAM
+#define RT_OPT_CAM 1  // A/B: one camera pass for path starts without a buffered sample and buffer refills
+#endif
 typedef __attribute__((address_space(3))) double LdsDouble;
 typedef __attribute__((address_space(3))) int32_t LdsInt;
 typedef __attribute__((address_space(3))) uint64_t LdsU64;
@@ -75,6 +78,42 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
         RT_DBG_REGION(0);
         RT_DBG_TSTART(t_it);
         bool done = false;
+#if RT_OPT_CAM
+        // camera: a lane starting a path takes its buffered sample, or joins the camera pass below
+        RT_DBG_TSTART(t_fr);
+        if (active && fresh && nvalid) {
+            RT_DBG_REGION(2);
+            begin_path(sc, CameraSample{v3(nbd[0], nbd[256], nbd[512]), nbr[0], nbr[256]}, ps);
+            fresh = false;
+            nvalid = false;
+        }
+        RT_DBG_TEND(1, t_fr);
+        RT_DBG_TSTART(t_rf);
+        // camera pass: lanes that start a path now without a buffered sample (sample s), plus lanes
+        // with a path in progress and a next sample in the same subpixel (sample s + 1, buffered);
+        // run when any lane needs a sample now or >= refill lanes need a buffer
+        {
+            const bool now = active && fresh;
+            const bool need = active && !fresh && !nvalid && s + 1 < a.n_samples;
+            if (__any(now) || (refill > 0 && __popcll(__ballot(need)) >= refill)) {
+                if (now || (refill > 0 && need)) {
+                    RT_DBG_REGION(3);
+                    const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), now ? s : s + 1);
+                    if (now) {
+                        begin_path(sc, nb, ps);
+                        fresh = false;
+                    } else {
+                        nbd[0] = nb.d.x; nbd[256] = nb.d.y; nbd[512] = nb.d.z;
+                        nbr[0] = nb.r0; nbr[256] = nb.r1;
+                        nvalid = true;
+                    }
+                }
+            }
+        }
+        RT_DBG_TEND(4, t_rf);
+        if (active) {
+            RT_DBG_REGION(1);
+#else
         if (active) {
             RT_DBG_REGION(1);
             RT_DBG_TSTART(t_fr);
@@ -85,6 +124,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
                 nvalid = false;
             }
             RT_DBG_TEND(1, t_fr);
+#endif
             RT_DBG_TSTART(t_tr);
             HitRec hr = trace_closest<C>(sc, ps.ray);
             RT_DBG_TEND(2, t_tr);
@@ -108,6 +148,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
             }
             RT_DBG_TEND(6, t_se);
         }
+#if !RT_OPT_CAM
         RT_DBG_TSTART(t_rf);
         // refill pass: lanes with a path in progress and a next sample in the same subpixel
         const bool need = active && !fresh && !nvalid && s + 1 < a.n_samples;
@@ -120,7 +161,10 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderAr
                 nvalid = true;
             }
         }
+#endif
+#if !RT_OPT_CAM
         RT_DBG_TEND(4, t_rf);
+#endif
         RT_DBG_TSTART(t_bk);
         // cancellation (RenderJob::stop, server.rs:201-203): checked when a lane would start a new
         // subpixel; a set flag stops handing out work, lanes finish the subpixel they hold

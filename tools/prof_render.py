@@ -17,4 +17,4 @@ dt = time.perf_counter() - t
 n = w * h * 4 * (spp // 4)
 print(f"{scene} {w}x{h}x{spp} {mode}{' mis' if mis else ''}: {dt*1e3:.1f} ms wall, {st['device_ms']:.1f} ms device, "
       f"{n / st['device_ms'] / 1e3:.1f} Msamples/s, {st['vertices'] / max(1, n):.3f} vertices/sample, "
-      f"iterations {st['iterations']}")
+      f"iterations {st['iterations']}, rgb sha1 {__import__('hashlib').sha1(rgb.tobytes()).hexdigest()[:12]}")
