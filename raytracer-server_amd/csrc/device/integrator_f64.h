@@ -189,7 +189,7 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
                 if (defer) {
                     // mutually_visible (scene.rs:258-270) split: analytic objects now, meshes deferred
                     const RayInv inv = make_inv(sr.d);
-                    vis = visible_analytic<C>(sc, sr, inv, dist) ? 1. : 0.;
+                    vis = visible_analytic<C>(sc, y, sr, inv, dist) ? 1. : 0.;
                     if (vis > 0. && mesh_candidate<C>(sc, sr, inv, dist)) {
                         defer->pending = true;
                         defer->o = sr.o;
@@ -197,11 +197,11 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
                         defer->dist = dist;
                     }
                 } else {
-                    vis = visible_ray<C>(sc, sr, dist) ? 1. : 0.;
+                    vis = visible_ray<C>(sc, y, sr, dist) ? 1. : 0.;
                 }
             } else {
                 RT_DBG_TSTART(t_vi);
-                vis = visible_ray<C>(sc, sr, dist) ? 1. : 0.;
+                vis = visible_ray<C>(sc, y, sr, dist) ? 1. : 0.;
                 RT_DBG_TEND(10, t_vi);
             }
             V3 c;

@@ -737,18 +737,42 @@ RT_DEV void surface(const DevScene& sc, const Ray& ray, const HitRec& h, V3* pos
 // rounds monotonically). Analytic objects are tested before meshes (order-free for a boolean).
 // r = {x, norm(y - x)} and dist = mag(y - x) as the caller computed them (visible() below, or the
 // NEE term's own values: same bits).
+//
+// Axis planes: a plane with both endpoints strictly on one side cannot block (exact; DESIGN.md §2:
+// behind x its t < 0, beyond y its t >= |y - x| (1 - 2^-52) and t + 0.001 >= |y - x| for
+// |y - x| < 1e9), so the exact plane test (and the ray reciprocals it needs) runs only for lanes
+// whose segment crosses or touches a plane.
+template <int K>
+RT_DEV bool planes_clear(CTab* T, double xk, double yk) {
+    bool c = true;
+#pragma unroll
+    for (int i = 0; i < kMaxAxisPlanes; ++i) {
+        if (i < T->n_ax[K]) {
+            const double p = T->ax_pos[K][i];
+            c &= (xk < p && yk < p) || (xk > p && yk > p);
+        }
+    }
+    return c;
+}
 template <class C>
-RT_DEV bool visible_ray(const DevScene& sc, const Ray& r, double dist) {
+RT_DEV bool visible_ray(const DevScene& sc, V3 y, const Ray& r, double dist) {
     RT_DBG_REGION(13);
     CTab* T = tables(sc);
     const double ERR_MARGIN = 0.001;
-    const RayInv inv = make_inv(r.d);
     if constexpr (C::compact) {
         bool occluded = false;
         auto visit = [&](double t, int, int) { occluded |= !(t + ERR_MARGIN >= dist); };
-        axis_planes<0>(sc, T, r, inv, visit);
-        axis_planes<1>(sc, T, r, inv, visit);
-        axis_planes<2>(sc, T, r, inv, visit);
+        const bool clear = dist < 1e9 && planes_clear<0>(T, r.o.x, y.x) && planes_clear<1>(T, r.o.y, y.y) &&
+                           planes_clear<2>(T, r.o.z, y.z);
+        RayInv inv;
+        const bool gen = T->n_gen > 0;  // the generic intersectors use the reciprocals too
+        if (gen) inv = make_inv(r.d);
+        if (!clear) {
+            if (!gen) inv = make_inv(r.d);
+            axis_planes<0>(sc, T, r, inv, visit);
+            axis_planes<1>(sc, T, r, inv, visit);
+            axis_planes<2>(sc, T, r, inv, visit);
+        }
 #pragma unroll
         for (int i = 0; i < kMaxSpheres; ++i) {
             double t;
@@ -763,6 +787,7 @@ RT_DEV bool visible_ray(const DevScene& sc, const Ray& r, double dist) {
         }
         return true;
     }
+    const RayInv inv = make_inv(r.d);
     for (int pass = 0; pass < (C::mesh ? 2 : 1); ++pass) {
         for (int i = 0; i < sc.n_objects; ++i) {
             const DevObject& o = sc.objects[i];
@@ -774,11 +799,12 @@ RT_DEV bool visible_ray(const DevScene& sc, const Ray& r, double dist) {
     }
     return true;
 }
+
 template <class C>
 RT_DEV bool visible(const DevScene& sc, V3 x, V3 y) {
     V3 diff = y - x;
     double dist = mag(diff);
-    return visible_ray<C>(sc, Ray{x, diff / dist}, dist);  // norm(diff), sharing the magnitude
+    return visible_ray<C>(sc, y, Ray{x, diff / dist}, dist);  // norm(diff), sharing the magnitude
 }
 
 // ---- pieces of trace_ray / mutually_visible for the wavefront's deferred mesh queries ----
@@ -833,14 +859,18 @@ RT_DEV bool mesh_candidate(const DevScene& sc, const Ray& ray, const RayInv& inv
 }
 // mutually_visible split: the analytic objects here, the meshes later (mesh_occludes).
 template <class C>
-RT_DEV bool visible_analytic(const DevScene& sc, const Ray& r, const RayInv& inv, double dist) {
+RT_DEV bool visible_analytic(const DevScene& sc, V3 y, const Ray& r, const RayInv& inv, double dist) {
     CTab* T = tables(sc);
     const double ERR_MARGIN = 0.001;
     bool occluded = false;
     auto visit = [&](double t, int, int) { occluded |= !(t + ERR_MARGIN >= dist); };
-    axis_planes<0>(sc, T, r, inv, visit);
-    axis_planes<1>(sc, T, r, inv, visit);
-    axis_planes<2>(sc, T, r, inv, visit);
+    const bool clear = dist < 1e9 && planes_clear<0>(T, r.o.x, y.x) && planes_clear<1>(T, r.o.y, y.y) &&
+                       planes_clear<2>(T, r.o.z, y.z);
+    if (!clear) {
+        axis_planes<0>(sc, T, r, inv, visit);
+        axis_planes<1>(sc, T, r, inv, visit);
+        axis_planes<2>(sc, T, r, inv, visit);
+    }
 #pragma unroll
     for (int i = 0; i < kMaxSpheres; ++i) {
         double t;
