@@ -34,9 +34,20 @@ RT_DEV V3 operator*(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
 // ---- correctly rounded division with a shared divisor ----
 // q = RN(a / b) from y = RN(1 / b): q0 = RN(a y), r = a - b q0 (exact, FMA), q = RN(q0 + r y)
 // (Markstein's theorem; valid without overflow/underflow). Used only when |b| is in
-// [2^-900, 2^900]; otherwise, and for NaN/inf, the plain IEEE division is taken. r == 0 means q0
-// is the exact quotient (keeps the sign of a zero quotient). Bit-identical to a / b.
+// [2^-900, 2^900]; otherwise, and for NaN/inf, the plain IEEE division is taken. The sign of a
+// zero quotient is restored from q0 (see qdiv). Bit-identical to a / b for finite a.
+#ifndef RT_OPT_VOTE
+#define RT_OPT_VOTE 1
+#endif
 RT_DEV bool rcp_safe(double b) { return fabs(b) >= 0x1p-900 && fabs(b) <= 0x1p900; }
+// All active lanes satisfy p (a wave vote kept in SGPRs: ballot vs exec, no VGPR round trip).
+RT_DEV bool wave_all(bool p) {
+#if RT_OPT_VOTE
+    return __builtin_amdgcn_ballot_w64(p) == __builtin_amdgcn_read_exec();
+#else
+    return __all(p);
+#endif
+}
 // RN(1 / b) for rcp_safe(b): the compiler's own IEEE f64 division sequence for 1.0 / b (v_rcp_f64,
 // two Newton steps, residual correction) without its range scaling (v_div_scale) and special-case
 // fixup (v_div_fixup), both identities in that range (every intermediate stays normal). 7 VALU
@@ -50,13 +61,23 @@ RT_DEV double rcp_rn(double b) {
     e = fma(-b, r, 1.0);
     return fma(e, r, r);
 }
+#ifndef RT_OPT_QDIV
+#define RT_OPT_QDIV 1  // A/B: sign of a zero quotient by copysign (1) or by a select on r == 0 (0)
+#endif
 RT_DEV double qdiv(double a, double b, double y) {
     double q0 = a * y;
     double r = fma(-b, q0, a);
+#if RT_OPT_QDIV
+    // fma(r, y, q0) is RN(a / b); only a zero quotient (a = +-0) can come out with the wrong sign
+    // (+0 + -0 = +0), and q0 = a y already carries the quotient's sign whenever a != 0 (no
+    // underflow in range), so the sign bit is taken from q0 (one v_bfi_b32 instead of cmp + 2 selects).
+    return __builtin_copysign(fma(r, y, q0), q0);
+#else
     return r == 0.0 ? q0 : fma(r, y, q0);
+#endif
 }
 RT_DEV V3 operator/(V3 a, double s) {
-    if (__all(rcp_safe(s))) {  // wave-uniform: no per-lane exec juggling on the common path
+    if (wave_all(rcp_safe(s))) {  // wave-uniform: no per-lane exec juggling on the common path
         double y = rcp_rn(s);
         return v3(qdiv(a.x, s, y), qdiv(a.y, s, y), qdiv(a.z, s, y));
     }
@@ -138,7 +159,7 @@ struct RayInv {
 };
 RT_DEV RayInv make_inv(const V3& d) {
     RayInv v;
-    if (__all(rcp_safe(d.x) && rcp_safe(d.y) && rcp_safe(d.z))) {  // wave-uniform fast path
+    if (wave_all(rcp_safe(d.x) && rcp_safe(d.y) && rcp_safe(d.z))) {  // wave-uniform fast path
         v.rx = rcp_rn(d.x);
         v.ry = rcp_rn(d.y);
         v.rz = rcp_rn(d.z);
@@ -234,7 +255,7 @@ RT_DEV bool tri_t(const DevTri& tr, const Ray& ray, double* tout) {
     double det = det3(nd, ab, ac);
     double tn = det3(b, ab, ac), un = det3(nd, b, ac), vn = det3(nd, ab, b);
     double t, u, v;
-    if (__all(rcp_safe(det))) {  // wave-uniform
+    if (wave_all(rcp_safe(det))) {  // wave-uniform
         double y = rcp_rn(det);
         t = qdiv(tn, det, y);
         u = qdiv(un, det, y);
@@ -638,6 +659,8 @@ RT_DEV void consider(HitRec& h, double t, int idx, int prim) {
     if (h.obj < 0 || t < h.t || (t == h.t && idx < h.obj)) { h.t = t; h.obj = idx; h.prim = prim; }
 }
 // Sphere test on the compact table (same operations as sphere_t; r*r precomputed exactly).
+// (Conservative culls of spheres beyond tmax / below eps before the square root measured 4% slower
+// on cornell_box: the extra compares cost more than the divergent roots they skip.)
 template <class P>
 RT_DEV bool sphere_c(P c, const Ray& ray, double* tout) {
     V3 op = v3(c[0], c[1], c[2]) - ray.o;
