@@ -170,7 +170,7 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
 #if RT_OPT_VIS
         // norm(y - x) and |y - x| exactly as mutually_visible computes them (scene.rs:258-262): the
         // shadow ray reuses them
-        const double dist = sqrt(r_sqr);  // == mag(diff)
+        const double dist = sqrt_rn(r_sqr);  // == mag(diff)
         const V3 i = diff / dist;          // == norm(diff)
 #else
         const V3 i = norm(diff);

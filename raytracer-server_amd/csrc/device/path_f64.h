@@ -83,10 +83,33 @@ RT_DEV V3 operator/(V3 a, double s) {
     }
     return v3(a.x / s, a.y / s, a.z / s);
 }
+#ifndef RT_OPT_SQRT
+#define RT_OPT_SQRT 1  // A/B: unscaled sqrt sequence behind a wave vote (1) or the library sqrt (0)
+#endif
+// RN(sqrt(x)): for x in [2^-767, inf) the compiler's own f64 sqrt sequence (v_rsq_f64, one
+// Goldschmidt step and two Newton corrections) without its input scaling (an identity in that
+// range: ldexp by 0) and its 0/inf fixup (unreachable there); 11 VALU instead of 17. Other inputs
+// (0, tiny, inf, NaN, negative) take the library sqrt.
+RT_DEV double sqrt_rn(double x) {
+#if RT_OPT_SQRT
+    if (wave_all(x >= 0x1p-767 && x < INFINITY)) {
+        const double y = __builtin_amdgcn_rsq(x);
+        double g = x * y, h = y * 0.5;
+        const double r = fma(-h, g, 0.5);
+        g = fma(g, r, g);
+        h = fma(h, r, h);
+        double d = fma(-g, g, x);
+        g = fma(d, h, g);
+        d = fma(-g, g, x);
+        return fma(d, h, g);
+    }
+#endif
+    return sqrt(x);
+}
 RT_DEV double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 RT_DEV V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
 RT_DEV V3 mult(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
-RT_DEV double mag(V3 a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+RT_DEV double mag(V3 a) { return sqrt_rn(a.x * a.x + a.y * a.y + a.z * a.z); }
 RT_DEV V3 norm(V3 a) { return a / mag(a); }
 RT_DEV bool equal_within(V3 a, V3 b, double e) {
     return fabs(a.x - b.x) < e && fabs(a.y - b.y) < e && fabs(a.z - b.z) < e;
@@ -218,7 +241,7 @@ RT_DEV bool sphere_t(const DevObject& o, const Ray& ray, double* tout) {
     double b = dot(op, ray.d);
     double det = b * b - dot(op, op) + o.r * o.r;
     if (det < 0.) return false;
-    det = sqrt(det);
+    det = sqrt_rn(det);
     double t = b - det;
     if (t > eps) { *tout = t; return true; }
     t = b + det;
@@ -668,7 +691,7 @@ RT_DEV bool sphere_c(P c, const Ray& ray, double* tout) {
     double det = b * b - dot(op, op) + c[3];
     if (det < 0.) return false;
     RT_DBG_REGION(11);
-    det = sqrt(det);
+    det = sqrt_rn(det);
     double t = b - det;
     if (t > 1e-4) { *tout = t; return true; }
     t = b + det;
@@ -944,8 +967,8 @@ RT_DEV void local_coord(V3 n, V3* u, V3* v, V3* w) {
 template <class C>
 RT_DEV void brdf_sample(const DevObject& o, V3 n, V3 out, Rng& rng, V3* in, double* pdf) {
     if (o.brdf == BRDF_DIFFUSE) {
-        double z = sqrt(rng.uniform());
-        double r = sqrt(1.0 - z * z);
+        double z = sqrt_rn(rng.uniform());
+        double r = sqrt_rn(1.0 - z * z);
         double phi = 2.0 * PI * rng.uniform();
         double sphi, cphi;
         sincos_2pi(phi, &sphi, &cphi);
@@ -994,8 +1017,9 @@ RT_DEV void light_sample(const DevScene& sc, Rng& rng, V3* y, V3* ny, double* pd
         double z = 2. * xi1 - 1.;
         double sp, cp;
         sincos_2pi(2. * PI * xi2, &sp, &cp);
-        double x = sqrt(1.0 - z * z) * cp;
-        double yy = sqrt(1.0 - z * z) * sp;
+        const double sz = sqrt_rn(1.0 - z * z);
+        double x = sz * cp;
+        double yy = sz * sp;
         V3 n = norm(v3(x, yy, z));
         *y = ld3(L.pos) + n * L.r;
         *ny = n;

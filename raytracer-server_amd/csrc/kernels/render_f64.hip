@@ -51,10 +51,28 @@ typedef __attribute__((address_space(3))) double LdsDouble;
 typedef __attribute__((address_space(3))) int32_t LdsInt;
 typedef __attribute__((address_space(3))) uint64_t LdsU64;
 
+#ifndef RT_OPT_LDSOBJ
+#define RT_OPT_LDSOBJ 1  // A/B: the object table in LDS (per-lane object reads as ds_read)
+#endif
+
 template <int F, int W>
-__global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
+__global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
                                                           uint32_t* next_sub, long nsub, int refill) {
     using C = Cfg<F>;
+    // Compact scenes (<= kMaxCompactObjects objects): the object table is copied into LDS, so the
+    // shading's per-lane object reads (hit object, light) are ds_reads instead of global loads.
+    DevScene sc = sc_g;
+#if RT_OPT_LDSOBJ
+    __shared__ DevObject s_objs[C::compact ? kMaxCompactObjects : 1];
+    if constexpr (C::compact) {
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(sc_g.objects);
+        uint64_t* dst = reinterpret_cast<uint64_t*>(s_objs);
+        const int nw = sc_g.n_objects * (int)(sizeof(DevObject) / 8);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+        sc.objects = s_objs;
+    }
+#endif
     // Rarely touched per-lane state lives in LDS (one column per thread; VGPRs are the limit at 4
     // waves/SIMD): the subpixel accumulator (once per sample) and the camera-sample buffer — the
     // next sample's camera ray + RNG state, computed ahead in a pass the whole wave runs once
@@ -477,6 +495,9 @@ static int env_int(const char* name, int dflt) {
     return v ? std::atoi(v) : dflt;
 }
 
+#ifndef RT_MK_W4
+#define RT_MK_W4 4  // waves/SIMD of the analytic-scene kernel (A/B builds: -DRT_MK_W4=5)
+#endif
 template <int F, int W>
 static void launch_mk(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
                       int refill, hipStream_t st) {
@@ -524,7 +545,7 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double
 #define RT_MK_CASE(F)                                                           \
     case F:                                                                     \
         if (waves == 3) launch_mk<F, 3>(sc, a, sub_buf, next_sub, nsub, refill, st);    \
-        else launch_mk<F, 4>(sc, a, sub_buf, next_sub, nsub, refill, st);               \
+        else launch_mk<F, RT_MK_W4>(sc, a, sub_buf, next_sub, nsub, refill, st);        \
         break;
     switch (a.features & 15) {
         RT_MK_CASE(0) RT_MK_CASE(1) RT_MK_CASE(2) RT_MK_CASE(3) RT_MK_CASE(4) RT_MK_CASE(5) RT_MK_CASE(6)

@@ -178,7 +178,7 @@ void pack_scene(rt_scene* s) {
 // Groups objects for the compact trace (axis planes per axis, spheres, everything else).
 void fill_compact(const Packed& p, rt::CompactTab* ds, int32_t* compact) {
     int nax[3] = {0, 0, 0}, ns = 0, ng = 0;
-    bool ok = true;
+    bool ok = p.objects.size() <= (size_t)rt::kMaxCompactObjects;
     for (size_t i = 0; i < p.objects.size(); ++i) {
         const rt::DevObject& o = p.objects[i];
         if (o.geom == rt::GEOM_PLANE && o.axis >= 0) {
