@@ -65,7 +65,7 @@ struct DevTri {
 constexpr int kMaxAxisPlanes = 4;  // per axis
 constexpr int kMaxSpheres = 4;
 constexpr int kMaxGeneric = 8;     // meshes and non-axis planes
-constexpr int kMaxCompactObjects = 32;  // compact scenes also hold their object table in LDS
+constexpr int kMaxCompactObjects = 16;  // compact scenes also hold their object table in LDS (3.3 KB)
 // The compact tables live in device memory (part of the scene blob) and are read through a
 // constant-address-space pointer: scalar loads at each use, so they never occupy SGPRs across the
 // path loop (as kernel arguments they did, and the spilled SGPRs were reloaded with ~900 static

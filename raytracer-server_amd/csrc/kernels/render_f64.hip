@@ -289,11 +289,24 @@ RT_DEV void park_query(const Park& p, const Ray& r, const RayInv& wi, double wt,
 }
 
 template <int F, int W>
-__global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
+__global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
                                                                uint32_t* next_sub, long nsub, int ksteps, int wmin,
                                                                int refill) {
     using C = Cfg<F>;
     static_assert(C::mesh && C::compact, "mesh megakernel needs the compact tables");
+    // object table in LDS, as in k_megakernel_f64 (2 blocks per CU: 2 x 78 KB of LDS)
+    DevScene sc = sc_g;
+#if RT_OPT_LDSOBJ
+    __shared__ DevObject s_objs[kMaxCompactObjects];
+    {
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(sc_g.objects);
+        uint64_t* dst = reinterpret_cast<uint64_t*>(s_objs);
+        const int nw = sc_g.n_objects * (int)(sizeof(DevObject) / 8);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+        sc.objects = s_objs;
+    }
+#endif
     __shared__ double s_park_d[kParkD * kParkThreads];
     __shared__ int32_t s_park_i[kParkI * kParkThreads];
     const Park park{(LdsDouble*)s_park_d + threadIdx.x, (LdsInt*)s_park_i + threadIdx.x};
