@@ -15,7 +15,11 @@ struct RenderArgs {
     int32_t features;  // Cfg<F> bits: 1 mesh, 2 phong, 4 mis (kernel specialisation)
     int32_t mesh_nodes;  // octree nodes of the largest mesh (megakernel choice)
     int32_t row_step;    // tile row i = screen row y0 + i * row_step
-    int32_t pad1;
+    int32_t tail_cps;    // split tail: chunks per subpixel
+    // split tail (megakernels): subpixels [n_whole, nsub) are handed out as chunks of 2^chunk_lg
+    // samples; a chunk's lane stores each sample's radiance in tail_buf[sub - n_whole][sample][3]
+    // and k_tail_sum adds them up in sample order afterwards (the same sequential sum)
+    int32_t n_whole, chunk_lg;
     uint64_t seed;
     double cx[3], cy[3];  // camera frame (server.rs:330-331), computed on the host
     double inv_n;         // 1.0 / n_samples (server.rs:358)
@@ -23,10 +27,12 @@ struct RenderArgs {
     uint8_t* rgb_out;     // [pix][3]
     unsigned long long* counters;  // optional [0] = path vertices
     const int32_t* cancel;         // optional device view of the host cancel flag (mapped memory)
+    double* tail_buf;              // split-tail sample radiance (see n_whole)
 };
 
+// tail_buf / tail_cap: scratch for the split tail (bytes); the launcher sizes the tail to fit it.
 hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
-                                 hipStream_t st);
+                                 double* tail_buf, size_t tail_cap, hipStream_t st);
 hipError_t launch_finalize_f64(const RenderArgs& a, const double* sub_buf, hipStream_t st);
 hipError_t launch_trace_f64(const DevScene& sc, long n, const double* o, const double* d, double* t, int32_t* obj,
                             double* pos, double* nrm, hipStream_t st);

@@ -38,6 +38,25 @@ __device__ __forceinline__ void flush_count(unsigned long long* counter, uint32_
     n = 0;
 }
 
+// Work unit of ticket t: subpixel t whole (t < n_whole: samples [0, n)), or chunk c = t - n_whole of
+// the split tail (subpixel n_whole + c / cps, samples [k 2^chunk_lg, (k + 1) 2^chunk_lg), k = c % cps).
+__device__ __forceinline__ void unit_of(const RenderArgs& a, long t, int& id, int& s) {
+    if (t < a.n_whole) {
+        id = (int)t;
+        s = 0;
+    } else {
+        const uint32_t c = (uint32_t)(t - a.n_whole);  // < n_split * cps < 2^32 (plan_tail)
+        const uint32_t q = c / (uint32_t)a.tail_cps;
+        id = a.n_whole + (int)q;
+        s = (int)(c - q * (uint32_t)a.tail_cps) << a.chunk_lg;
+    }
+}
+// Is sample s + 1 still part of the unit that holds sample s? (No register for the unit's end: a
+// split unit ends at the next multiple of 2^chunk_lg.)
+__device__ __forceinline__ bool unit_has_next(const RenderArgs& a, int id, int s) {
+    return s + 1 < a.n_samples && (id < a.n_whole || ((s + 1) >> a.chunk_lg) == (s >> a.chunk_lg));
+}
+
 // Persistent megakernel: a resident grid whose lanes pull subpixels from a global counter. A lane
 // walks the spp/4 sample paths of its subpixel vertex by vertex; when a path ends, the next sample
 // starts in the same iteration (regeneration); when the subpixel is done its mean goes to
@@ -85,10 +104,14 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
     LdsU64* nbr = (LdsU64*)s_nbr + threadIdx.x;
     RT_DBG_TINIT();
     uint32_t nverts = 0;
-    long id = wave_ticket(next_sub, true);
-    bool active = id < nsub;
+    // tickets: whole subpixels, then the split tail's chunks (unit_of)
+    const long n_split = nsub - a.n_whole;
+    const long nunits = a.n_whole + n_split * a.tail_cps;
+    int id, s;  // subpixel (tile-local, < 2^31: rt_api.cpp check_params) and sample of the unit in hand
+    const long t0 = wave_ticket(next_sub, true);
+    unit_of(a, t0, id, s);
+    bool active = t0 < nunits;
     acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
-    int s = 0;
     PathState ps;
     bool fresh = true;
     bool nvalid = false;
@@ -112,7 +135,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
         // run when any lane needs a sample now or >= refill lanes need a buffer
         {
             const bool now = active && fresh;
-            const bool need = active && !fresh && !nvalid && s + 1 < a.n_samples;
+            const bool need = active && !fresh && !nvalid && unit_has_next(a, id, s);
             if (__any(now) || (refill > 0 && __popcll(__ballot(need)) >= refill)) {
                 if (now || (refill > 0 && need)) {
                     RT_DBG_REGION(3);
@@ -153,23 +176,32 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
             RT_DBG_TSTART(t_se);
             if (fresh) {
                 RT_DBG_REGION(4);
-                V3 acc = v3(acc_l[0], acc_l[256], acc_l[512]);
-                acc = acc + ps.L * a.inv_n;  // server.rs:357-358
-                acc_l[0] = acc.x; acc_l[256] = acc.y; acc_l[512] = acc.z;
-                if (++s == a.n_samples) {
-                    double* o = sub_buf + (size_t)id * 3;
-                    o[0] = acc.x;
-                    o[1] = acc.y;
-                    o[2] = acc.z;
-                    done = true;
+                if (id < a.n_whole) {
+                    V3 acc = v3(acc_l[0], acc_l[256], acc_l[512]);
+                    acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                    acc_l[0] = acc.x; acc_l[256] = acc.y; acc_l[512] = acc.z;
+                    if (++s == a.n_samples) {
+                        double* o = sub_buf + (size_t)id * 3;
+                        o[0] = acc.x;
+                        o[1] = acc.y;
+                        o[2] = acc.z;
+                        done = true;
+                    }
+                } else {  // split tail: the sample's radiance, summed in order by k_tail_sum_f64
+                    double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
+                    o[0] = ps.L.x;
+                    o[1] = ps.L.y;
+                    o[2] = ps.L.z;
+                    done = !unit_has_next(a, id, s);
+                    ++s;
                 }
             }
             RT_DBG_TEND(6, t_se);
         }
 #if !RT_OPT_CAM
         RT_DBG_TSTART(t_rf);
-        // refill pass: lanes with a path in progress and a next sample in the same subpixel
-        const bool need = active && !fresh && !nvalid && s + 1 < a.n_samples;
+        // refill pass: lanes with a path in progress and a next sample in the same unit
+        const bool need = active && !fresh && !nvalid && unit_has_next(a, id, s);
         if (refill > 0 && __popcll(__ballot(need)) >= refill) {
             if (need) {
                 RT_DBG_REGION(3);
@@ -188,13 +220,12 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
         // subpixel; a set flag stops handing out work, lanes finish the subpixel they hold
         bool stop = false;
         if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
-        long nid = wave_ticket(next_sub, done && !stop);
+        const long nt = wave_ticket(next_sub, done && !stop);
         if (__any(done)) flush_count(a.counters, nverts);  // keeps the 32-bit lane counts far from overflow
         if (done) {
-            id = stop ? nsub : nid;
-            active = id < nsub;
+            unit_of(a, nt, id, s);
+            active = !stop && nt < nunits;
             acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
-            s = 0;
             fresh = true;
             nvalid = false;
         }
@@ -458,6 +489,25 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     flush_count(a.counters, nverts);
 }
 
+// Split tail: subpixel n_whole + j's mean from its samples' radiance, summed in sample order
+// exactly as the megakernel's in-register accumulator (acc = acc + L * inv_n, server.rs:357-358).
+// tail_buf is subpixel-major ([j][sample][3]): a chunk's lane writes one contiguous run (the
+// sample-major layout scattered every write over the whole buffer: TLB misses, 2x slower tail).
+__global__ __launch_bounds__(256) void k_tail_sum_f64(RenderArgs a, double* __restrict__ sub_buf, long n_split) {
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long j = (long)blockIdx.x * blockDim.x + threadIdx.x; j < n_split; j += stride) {
+        V3 acc = v3(0.0, 0.0, 0.0);
+        for (int s = 0; s < a.n_samples; ++s) {
+            const double* L = a.tail_buf + ((size_t)j * (size_t)a.n_samples + (size_t)s) * 3;
+            acc = acc + v3(L[0], L[1], L[2]) * a.inv_n;
+        }
+        double* o = sub_buf + (size_t)(a.n_whole + j) * 3;
+        o[0] = acc.x;
+        o[1] = acc.y;
+        o[2] = acc.z;
+    }
+}
+
 // 4 subpixel means -> RGB8 (server.rs:360 clamp-then-average, :366-368 gamma, :187-189 `as u8`).
 __global__ __launch_bounds__(256) void k_finalize_f64(RenderArgs a, const double* __restrict__ sub_buf) {
     const long npix = (long)a.tw * a.th;
@@ -511,12 +561,43 @@ static int env_int(const char* name, int dflt) {
 #ifndef RT_MK_W4
 #define RT_MK_W4 4  // waves/SIMD of the analytic-scene kernel (A/B builds: -DRT_MK_W4=5)
 #endif
+// Split tail (RenderArgs::n_whole): the last subpixels are handed out in chunks of samples, so the
+// frame does not end with lanes idling while others finish a whole subpixel (the 1/N-sized frames
+// of an N-GPU run hold only a few subpixels per lane). Up to one subpixel per resident lane is
+// split, limited by the scratch buffer (tail_cap bytes); RT_MK_TAIL=0 disables it.
+static void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_buf, size_t tail_cap) {
+    static const int tail_env = env_int("RT_MK_TAIL", 1);
+    const size_t per_sub = (size_t)std::max(0, a.n_samples) * 3 * sizeof(double);
+    long n_split = 0;
+    if (tail_env && tail_buf && a.n_samples >= 64 && per_sub > 0)
+        n_split = std::min({lanes, nsub / 2, (long)(tail_cap / per_sub)});
+    a.n_whole = (int32_t)(nsub - n_split);
+    // chunks of 2^chunk_lg samples, about RT_MK_TAIL_CPS (4) per subpixel: every chunk costs a
+    // ticket on the one global counter, and short chunks make those atomics the bottleneck of the
+    // tail (16 per subpixel measured 11% slower on the whole frame)
+    // ... and at least 32 samples (≈500 wave iterations): shorter chunks turn over so often that the
+    // counter's atomics saturate (8-sample chunks at 256 spp: the tail ran at a third of the speed)
+    static const int cps_target = std::max(1, env_int("RT_MK_TAIL_CPS", 4));
+    a.chunk_lg = 5;
+    while ((a.n_samples >> a.chunk_lg) > cps_target) ++a.chunk_lg;
+    a.tail_cps = (a.n_samples + (1 << a.chunk_lg) - 1) >> a.chunk_lg;
+    if (a.tail_cps < 2) a.n_whole = (int32_t)nsub;  // nothing to split
+    a.tail_buf = tail_buf;
+}
+
 template <int F, int W>
-static void launch_mk(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
-                      int refill, hipStream_t st) {
+static void launch_mk(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub, long nsub,
+                      int refill, double* tail_buf, size_t tail_cap, hipStream_t st) {
     const long blocks = resident_blocks(k_megakernel_f64<F, W>, (nsub + 255) / 256);
+    RenderArgs a = a_in;
+    plan_tail(a, nsub, blocks * 256, tail_buf, tail_cap);
     hipLaunchKernelGGL((k_megakernel_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub, nsub,
                        refill);
+    const long n_split = nsub - a.n_whole;
+    if (n_split > 0) {
+        const long tb = std::max(1L, std::min(4096L, (n_split + 255) / 256));
+        hipLaunchKernelGGL(k_tail_sum_f64, dim3((unsigned)tb), dim3(256), 0, st, a, sub_buf, n_split);
+    }
 }
 template <int F, int W>
 static void launch_mm(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
@@ -526,8 +607,12 @@ static void launch_mm(const DevScene& sc, const RenderArgs& a, double* sub_buf, 
                        nsub, ksteps, wmin, refill);
 }
 
-hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
-                                 hipStream_t st) {
+hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub,
+                                 double* tail_buf, size_t tail_cap, hipStream_t st) {
+    RenderArgs a = a_in;
+    a.n_whole = (int32_t)((long)a.tw * a.th * 4);  // no split tail unless planned (analytic megakernel)
+    a.chunk_lg = 0;
+    a.tail_cps = 1;
     const long nsub = (long)a.tw * a.th * 4;
     if (nsub <= 0 || a.n_samples <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(next_sub, 0, sizeof(uint32_t), st);
@@ -557,8 +642,8 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double
     }
 #define RT_MK_CASE(F)                                                           \
     case F:                                                                     \
-        if (waves == 3) launch_mk<F, 3>(sc, a, sub_buf, next_sub, nsub, refill, st);    \
-        else launch_mk<F, RT_MK_W4>(sc, a, sub_buf, next_sub, nsub, refill, st);        \
+        if (waves == 3) launch_mk<F, 3>(sc, a, sub_buf, next_sub, nsub, refill, tail_buf, tail_cap, st);  \
+        else launch_mk<F, RT_MK_W4>(sc, a, sub_buf, next_sub, nsub, refill, tail_buf, tail_cap, st);      \
         break;
     switch (a.features & 15) {
         RT_MK_CASE(0) RT_MK_CASE(1) RT_MK_CASE(2) RT_MK_CASE(3) RT_MK_CASE(4) RT_MK_CASE(5) RT_MK_CASE(6)

@@ -48,12 +48,15 @@ struct Workspace {
     double* q2 = nullptr;        // [10][slots]: origin xyz, dir xyz, dist, weighted NEE term xyz
     double* sub_buf = nullptr; // subpixel means when the caller passes none
     size_t sub_cap = 0;
+    double* tail_buf = nullptr;  // megakernel split tail (bytes: tail_cap)
+    size_t tail_cap = 0;
     uint32_t* host_ctrl = nullptr;  // pinned mirror of ctrl
     hipEvent_t ev = nullptr;
 
     hipError_t ensure_counters();
     hipError_t ensure_slots(size_t n);
     hipError_t ensure_sub(size_t pixels);
+    hipError_t ensure_tail(size_t bytes);
     ~Workspace();
 };
 

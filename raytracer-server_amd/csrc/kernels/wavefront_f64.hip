@@ -466,6 +466,16 @@ hipError_t Workspace::ensure_sub(size_t pixels) {
     return e;
 }
 
+hipError_t Workspace::ensure_tail(size_t bytes) {
+    if (tail_cap >= bytes) return hipSuccess;
+    if (tail_buf) (void)hipFree(tail_buf);
+    tail_buf = nullptr;
+    tail_cap = 0;
+    hipError_t e = hipMalloc(&tail_buf, bytes);
+    if (e == hipSuccess) tail_cap = bytes;
+    return e;
+}
+
 hipError_t Workspace::ensure_slots(size_t n) {
     hipError_t e;
     if (!ctrl) {
@@ -519,6 +529,7 @@ Workspace::~Workspace() {
     if (blob) (void)hipFree(blob);
     if (ctrl) (void)hipFree(ctrl);
     if (sub_buf) (void)hipFree(sub_buf);
+    if (tail_buf) (void)hipFree(tail_buf);
     if (host_ctrl) (void)hipHostFree(host_ctrl);
     if (ev) (void)hipEventDestroy(ev);
 }

@@ -376,7 +376,13 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
         if (e == hipSuccess && a.n_samples <= 0) e = hipMemsetAsync(sub, 0, npix * 12 * sizeof(double), st);
         if (e == hipSuccess) {
             a.counters = stats ? ws->counters : nullptr;
-            e = rt::launch_megakernel_f64(ds, a, sub, (uint32_t*)(ws->counters + 4), st);
+            // split-tail scratch: up to one subpixel per resident lane, at most 1.5 GB
+            const size_t per_sub = (size_t)std::max(0, a.n_samples) * 3 * sizeof(double);
+            const size_t want = std::min<size_t>((size_t)3 << 29, per_sub * std::min<size_t>(npix * 4 / 2, (size_t)1 << 19));
+            if (per_sub > 0 && want >= per_sub) {
+                if (ws->ensure_tail(want) != hipSuccess) (void)hipGetLastError();  // no tail split then
+            }
+            e = rt::launch_megakernel_f64(ds, a, sub, (uint32_t*)(ws->counters + 4), ws->tail_buf, ws->tail_cap, st);
         }
         if (e == hipSuccess) e = rt::launch_finalize_f64(a, sub, st);
         if (e != hipSuccess) { out = RT_E_HIP; err = std::string("megakernel: ") + hipGetErrorString(e); }

@@ -94,6 +94,19 @@ def test_megakernel_equals_wavefront(rt, gpu_scenes):
         assert a[2]["vertices"] == b[2]["vertices"]
 
 
+def test_split_tail_equals_wavefront(rt, gpu_scenes):
+    """The megakernel hands out its last subpixels (up to one per resident lane, at most half the
+    frame) as chunks of samples and sums their stored radiance afterwards in sample order
+    (render_f64.hip: plan_tail, k_tail_sum_f64): the means must be the bits of the whole-subpixel
+    sum. 96 samples per subpixel = 3 chunks of 32; the wavefront sums every subpixel in one lane."""
+    for name in ("cornell_box", "cubes"):
+        for tile, step in [(None, 1), ((0, 1, 80, 20), 3)]:
+            a = rt.render(gpu_scenes[name], 80, 60, 384, SEED, tile=tile, row_step=step, want_sub=True, megakernel=True)
+            b = rt.render(gpu_scenes[name], 80, 60, 384, SEED, tile=tile, row_step=step, want_sub=True, megakernel=False)
+            assert np.array_equal(a[1], b[1]) and np.array_equal(a[0], b[0]), (name, tile)
+            assert a[2]["vertices"] == b[2]["vertices"]
+
+
 def test_tiling_invariance_and_determinism(rt, gpu_scenes):
     s = gpu_scenes["cubes"]
     w, h = 200, 150
