@@ -348,10 +348,14 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     LdsDouble* nbd = (LdsDouble*)s_nbd + threadIdx.x;
     LdsU64* nbr = (LdsU64*)s_nbr + threadIdx.x;
     uint32_t nverts = 0;
-    long id = wave_ticket(next_sub, true);
-    bool active = id < nsub;
+    // tickets: whole subpixels, then the split tail's chunks (unit_of), as in k_megakernel_f64
+    const long n_split = nsub - a.n_whole;
+    const long nunits = a.n_whole + n_split * a.tail_cps;
+    int id, s;
+    const long t0 = wave_ticket(next_sub, true);
+    unit_of(a, t0, id, s);
+    bool active = t0 < nunits;
     acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
-    int s = 0;
     PathState ps;
     bool fresh = true;
     bool nvalid = false;
@@ -449,22 +453,31 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                 if (!walking) sample_end = !cont;
             }
             if (sample_end) {
-                V3 acc = v3(acc_l[0], acc_l[256], acc_l[512]);
-                acc = acc + ps.L * a.inv_n;  // server.rs:357-358
-                acc_l[0] = acc.x; acc_l[256] = acc.y; acc_l[512] = acc.z;
                 fresh = true;
-                if (++s == a.n_samples) {
-                    double* o = sub_buf + (size_t)id * 3;
-                    o[0] = acc.x;
-                    o[1] = acc.y;
-                    o[2] = acc.z;
-                    done = true;
+                if (id < a.n_whole) {
+                    V3 acc = v3(acc_l[0], acc_l[256], acc_l[512]);
+                    acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                    acc_l[0] = acc.x; acc_l[256] = acc.y; acc_l[512] = acc.z;
+                    if (++s == a.n_samples) {
+                        double* o = sub_buf + (size_t)id * 3;
+                        o[0] = acc.x;
+                        o[1] = acc.y;
+                        o[2] = acc.z;
+                        done = true;
+                    }
+                } else {  // split tail (k_tail_sum_f64)
+                    double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
+                    o[0] = ps.L.x;
+                    o[1] = ps.L.y;
+                    o[2] = ps.L.z;
+                    done = !unit_has_next(a, id, s);
+                    ++s;
                 }
             }
         }
         // camera-sample refill pass: lanes with a path in progress (walking or not) and a next sample
-        // in the same subpixel
-        const bool need = active && !fresh && !nvalid && s + 1 < a.n_samples;
+        // in the same unit
+        const bool need = active && !fresh && !nvalid && unit_has_next(a, id, s);
         if (refill > 0 && __popcll(__ballot(need)) >= refill) {
             if (need) {
                 const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), s + 1);
@@ -475,13 +488,12 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
         }
         bool stop = false;
         if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
-        long nid = wave_ticket(next_sub, done && !stop);
+        const long nt = wave_ticket(next_sub, done && !stop);
         if (__any(done)) flush_count(a.counters, nverts);  // keeps the 32-bit lane counts far from overflow
         if (done) {
-            id = stop ? nsub : nid;
-            active = id < nsub;
+            unit_of(a, nt, id, s);
+            active = !stop && nt < nunits;
             acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
-            s = 0;
             fresh = true;
             nvalid = false;
         }
@@ -600,11 +612,18 @@ static void launch_mk(const DevScene& sc, const RenderArgs& a_in, double* sub_bu
     }
 }
 template <int F, int W>
-static void launch_mm(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
-                      int ksteps, int wmin, int refill, hipStream_t st) {
+static void launch_mm(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub, long nsub,
+                      int ksteps, int wmin, int refill, double* tail_buf, size_t tail_cap, hipStream_t st) {
     const long blocks = resident_blocks(k_megakernel_mesh_f64<F, W>, (nsub + 255) / 256);
+    RenderArgs a = a_in;
+    plan_tail(a, nsub, blocks * 256, tail_buf, tail_cap);
     hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub,
                        nsub, ksteps, wmin, refill);
+    const long n_split = nsub - a.n_whole;
+    if (n_split > 0) {
+        const long tb = std::max(1L, std::min(4096L, (n_split + 255) / 256));
+        hipLaunchKernelGGL(k_tail_sum_f64, dim3((unsigned)tb), dim3(256), 0, st, a, sub_buf, n_split);
+    }
 }
 
 hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub,
@@ -634,7 +653,7 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, dou
     if (interleave && (a.features & 9) == 9 && a.mesh_nodes >= interleave) {
 #define RT_MM_CASE(F)                                                        \
     case F:                                                                  \
-        launch_mm<F, 2>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, st);   \
+        launch_mm<F, 2>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, tail_buf, tail_cap, st); \
         break;
         switch (a.features & 15) { RT_MM_CASE(9) RT_MM_CASE(11) RT_MM_CASE(13) RT_MM_CASE(15) }
 #undef RT_MM_CASE

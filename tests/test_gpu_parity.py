@@ -98,8 +98,9 @@ def test_split_tail_equals_wavefront(rt, gpu_scenes):
     """The megakernel hands out its last subpixels (up to one per resident lane, at most half the
     frame) as chunks of samples and sums their stored radiance afterwards in sample order
     (render_f64.hip: plan_tail, k_tail_sum_f64): the means must be the bits of the whole-subpixel
-    sum. 96 samples per subpixel = 3 chunks of 32; the wavefront sums every subpixel in one lane."""
-    for name in ("cornell_box", "cubes"):
+    sum. 96 samples per subpixel = 3 chunks of 32; the wavefront sums every subpixel in one lane.
+    flying_unicorn runs the interleaved mesh megakernel, the others the analytic one."""
+    for name in ("cornell_box", "cubes", "flying_unicorn"):
         for tile, step in [(None, 1), ((0, 1, 80, 20), 3)]:
             a = rt.render(gpu_scenes[name], 80, 60, 384, SEED, tile=tile, row_step=step, want_sub=True, megakernel=True)
             b = rt.render(gpu_scenes[name], 80, 60, 384, SEED, tile=tile, row_step=step, want_sub=True, megakernel=False)
