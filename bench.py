@@ -95,6 +95,17 @@ def cpu_baseline(args):
                       f"({samples} samples, {dt:.1f} s, f64, CPU oracle restating server.rs:320-368 + scene.rs + geometry.rs)"}
 
 
+def load_valu(workload_key):
+    """VALU wave-instructions per path vertex of the dominant kernel, from the SQ PMC passes in
+    profiles/ (tools/gpu_pmc_mk.sh -> profiles/pmc_valu.json), or None."""
+    path = os.path.join(REPO, "profiles", "pmc_valu.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(workload_key)
+    except (OSError, ValueError):
+        return None
+
+
 def load_traffic(workload_key):
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
@@ -214,6 +225,15 @@ def main():
                          "alg_bytes_per_launch": alg_bytes,
                          "model": "SURVEY 8(d): 88 B/sample + 280 B/vertex (canonical f32 SoA wavefront state)"},
         }
+        # The megakernel's own bound is VALU issue: PMC instructions per vertex x the
+        # vertex rate of this run, against 1024 SIMDs x one wave-instruction per 4 cycles at 2.4 GHz
+        valu = load_valu(f"{args.scene} megakernel") if args.mode == "megakernel" else None
+        if valu:
+            rate = valu["valu_inst_per_vertex"] * st["vertices"] / (dev_ms / 1e3)
+            peak = 1024 * 2.4e9 / 4
+            out["roofline"]["valu"] = {"achieved": round(rate / 1e9, 2), "peak": round(peak / 1e9, 2),
+                                       "unit": "G wave-instr/s", "frac": round(rate / peak, 4),
+                                       "inst_per_vertex": valu["valu_inst_per_vertex"], "source": valu["source"]}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)

@@ -51,6 +51,10 @@ __device__ __forceinline__ void unit_of(const RenderArgs& a, long t, int& id, in
         s = (int)(c - q * (uint32_t)a.tail_cps) << a.chunk_lg;
     }
 }
+// Is sample s2 (> s) part of the unit that holds sample s?
+__device__ __forceinline__ bool unit_has(const RenderArgs& a, int id, int s, int s2) {
+    return s2 < a.n_samples && (id < a.n_whole || (s2 >> a.chunk_lg) == (s >> a.chunk_lg));
+}
 // Is sample s + 1 still part of the unit that holds sample s? (No register for the unit's end: a
 // split unit ends at the next multiple of 2^chunk_lg.)
 __device__ __forceinline__ bool unit_has_next(const RenderArgs& a, int id, int s) {
@@ -63,9 +67,10 @@ __device__ __forceinline__ bool unit_has_next(const RenderArgs& a, int id, int s
 // sub_buf (sequential sum in sample order, server.rs:338-358) and the lane takes the next
 // subpixel. Waves idle only in the frame's final tail, not per wave.
 // W = minimum waves per SIMD requested from the register allocator.
-#ifndef RT_OPT_CAM
-#define RT_OPT_CAM 1  // A/B: one camera pass for path starts without a buffered sample and buffer refills
+#ifndef RT_CAM_DEPTH
+#define RT_CAM_DEPTH 1  // camera samples buffered ahead per lane (k_megakernel_f64; 2 measured 1% slower)
 #endif
+constexpr int kCamDepth = RT_CAM_DEPTH;
 typedef __attribute__((address_space(3))) double LdsDouble;
 typedef __attribute__((address_space(3))) int32_t LdsInt;
 typedef __attribute__((address_space(3))) uint64_t LdsU64;
@@ -93,15 +98,15 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
     }
 #endif
     // Rarely touched per-lane state lives in LDS (one column per thread; VGPRs are the limit at 4
-    // waves/SIMD): the subpixel accumulator (once per sample) and the camera-sample buffer — the
-    // next sample's camera ray + RNG state, computed ahead in a pass the whole wave runs once
-    // >= refill lanes need one (begin_sample for the ~7% of lanes whose path ended each iteration
-    // otherwise runs every iteration at that lane utilisation).
-    __shared__ double s_acc[3 * 256], s_nbd[3 * 256];
-    __shared__ uint64_t s_nbr[2 * 256];
+    // waves/SIMD): the subpixel accumulator (once per sample) and the camera-sample buffer — a ring
+    // of kCamDepth next samples (camera ray + RNG state) per lane, computed ahead in passes the whole
+    // wave runs once >= refill lanes have a free slot (begin_sample for the ~7% of lanes whose path
+    // ended each iteration otherwise runs every iteration at that lane utilisation).
+    __shared__ double s_acc[3 * 256], s_nbd[kCamDepth * 3 * 256];
+    __shared__ uint64_t s_nbr[kCamDepth * 2 * 256];
     LdsDouble* acc_l = (LdsDouble*)s_acc + threadIdx.x;  // component k at [k * 256]
-    LdsDouble* nbd = (LdsDouble*)s_nbd + threadIdx.x;
-    LdsU64* nbr = (LdsU64*)s_nbr + threadIdx.x;
+    LdsDouble* nbd = (LdsDouble*)s_nbd + threadIdx.x;     // slot q, component k at [(q * 3 + k) * 256]
+    LdsU64* nbr = (LdsU64*)s_nbr + threadIdx.x;           // slot q, word k at [(q * 2 + k) * 256]
     RT_DBG_TINIT();
     uint32_t nverts = 0;
     // tickets: whole subpixels, then the split tail's chunks (unit_of)
@@ -114,39 +119,43 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
     acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
     PathState ps;
     bool fresh = true;
-    bool nvalid = false;
+    int nbuf = 0, hb = 0;  // buffered camera samples (s + 1 .. s + nbuf) and the ring's head slot
     while (__any(active)) {
         RT_DBG_REGION(0);
         RT_DBG_TSTART(t_it);
         bool done = false;
-#if RT_OPT_CAM
-        // camera: a lane starting a path takes its buffered sample, or joins the camera pass below
+        // camera: a lane starting a path takes its next buffered sample, or joins the camera pass
         RT_DBG_TSTART(t_fr);
-        if (active && fresh && nvalid) {
+        if (active && fresh && nbuf > 0) {
             RT_DBG_REGION(2);
-            begin_path(sc, CameraSample{v3(nbd[0], nbd[256], nbd[512]), nbr[0], nbr[256]}, ps);
+            const int q = hb * 3 * 256, r = hb * 2 * 256;
+            begin_path(sc, CameraSample{v3(nbd[q], nbd[q + 256], nbd[q + 512]), nbr[r], nbr[r + 256]}, ps);
             fresh = false;
-            nvalid = false;
+            hb = hb + 1 == kCamDepth ? 0 : hb + 1;
+            --nbuf;
         }
         RT_DBG_TEND(1, t_fr);
         RT_DBG_TSTART(t_rf);
         // camera pass: lanes that start a path now without a buffered sample (sample s), plus lanes
-        // with a path in progress and a next sample in the same subpixel (sample s + 1, buffered);
-        // run when any lane needs a sample now or >= refill lanes need a buffer
+        // with a free ring slot whose next sample (s + nbuf + 1) is in the same unit; run when any
+        // lane needs a sample now or >= refill lanes have a free slot
         {
             const bool now = active && fresh;
-            const bool need = active && !fresh && !nvalid && unit_has_next(a, id, s);
+            const bool need = active && !fresh && nbuf < kCamDepth && unit_has(a, id, s, s + nbuf + 1);
             if (__any(now) || (refill > 0 && __popcll(__ballot(need)) >= refill)) {
                 if (now || (refill > 0 && need)) {
                     RT_DBG_REGION(3);
-                    const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), now ? s : s + 1);
+                    const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), now ? s : s + nbuf + 1);
                     if (now) {
                         begin_path(sc, nb, ps);
                         fresh = false;
                     } else {
-                        nbd[0] = nb.d.x; nbd[256] = nb.d.y; nbd[512] = nb.d.z;
-                        nbr[0] = nb.r0; nbr[256] = nb.r1;
-                        nvalid = true;
+                        int slot = hb + nbuf;
+                        slot = slot >= kCamDepth ? slot - kCamDepth : slot;
+                        const int q = slot * 3 * 256, r = slot * 2 * 256;
+                        nbd[q] = nb.d.x; nbd[q + 256] = nb.d.y; nbd[q + 512] = nb.d.z;
+                        nbr[r] = nb.r0; nbr[r + 256] = nb.r1;
+                        ++nbuf;
                     }
                 }
             }
@@ -154,18 +163,6 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
         RT_DBG_TEND(4, t_rf);
         if (active) {
             RT_DBG_REGION(1);
-#else
-        if (active) {
-            RT_DBG_REGION(1);
-            RT_DBG_TSTART(t_fr);
-            if (fresh) {
-                RT_DBG_REGION(2);
-                if (nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[256], nbd[512]), nbr[0], nbr[256]}, ps);
-                else { RT_DBG_REGION(5); begin_sample(sc, a, subpixel_of(a, id), s, ps); }
-                nvalid = false;
-            }
-            RT_DBG_TEND(1, t_fr);
-#endif
             RT_DBG_TSTART(t_tr);
             HitRec hr = trace_closest<C>(sc, ps.ray);
             RT_DBG_TEND(2, t_tr);
@@ -198,23 +195,6 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
             }
             RT_DBG_TEND(6, t_se);
         }
-#if !RT_OPT_CAM
-        RT_DBG_TSTART(t_rf);
-        // refill pass: lanes with a path in progress and a next sample in the same unit
-        const bool need = active && !fresh && !nvalid && unit_has_next(a, id, s);
-        if (refill > 0 && __popcll(__ballot(need)) >= refill) {
-            if (need) {
-                RT_DBG_REGION(3);
-                const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), s + 1);
-                nbd[0] = nb.d.x; nbd[256] = nb.d.y; nbd[512] = nb.d.z;
-                nbr[0] = nb.r0; nbr[256] = nb.r1;
-                nvalid = true;
-            }
-        }
-#endif
-#if !RT_OPT_CAM
-        RT_DBG_TEND(4, t_rf);
-#endif
         RT_DBG_TSTART(t_bk);
         // cancellation (RenderJob::stop, server.rs:201-203): checked when a lane would start a new
         // subpixel; a set flag stops handing out work, lanes finish the subpixel they hold
@@ -227,7 +207,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
             active = !stop && nt < nunits;
             acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
             fresh = true;
-            nvalid = false;
+            nbuf = 0;
+            hb = 0;
         }
         RT_DBG_TEND(5, t_bk);
         RT_DBG_TEND(0, t_it);
