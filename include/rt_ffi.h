@@ -49,6 +49,9 @@ extern "C" {
 #define RT_FLAG_MIS (1u << 0)        /* config.toml `use_mis` (dead in the reference, scene.rs:188): build-defined balance heuristic */
 #define RT_FLAG_MEGAKERNEL (1u << 1) /* fused per-lane path loop instead of the wavefront pipeline */
 #define RT_FLAG_FP32 (1u << 2)       /* f32 arithmetic (statistical parity only); default is the reference's f64 */
+#define RT_FLAG_MESH_NEAREST (1u << 3) /* Mesh::intersect's `octree: None` branch (geometry.rs:886-903: nearest
+                                          triangle, strict < in index order) instead of the octree walk, accelerated on
+                                          the device by a BVH; megakernel only (RT_E_INVAL with the wavefront) */
 
 typedef struct rt_scene rt_scene;
 
@@ -137,6 +140,9 @@ int rt_render_device(const rt_scene* scene, const rt_render_params* params, void
 /* Scene::trace_ray on the device for n host rays: t, object id (-1: no hit), hit pos/normal. */
 int rt_trace_rays(const rt_scene* scene, int32_t device, int64_t n, const double* origins, const double* dirs,
                   double* t, int32_t* object, double* pos, double* normal);
+/* The same with render flags (RT_FLAG_MESH_NEAREST selects the nearest-triangle mesh semantics). */
+int rt_trace_rays_flags(const rt_scene* scene, int32_t device, uint32_t flags, int64_t n, const double* origins,
+                        const double* dirs, double* t, int32_t* object, double* pos, double* normal);
 
 const char* rt_last_error(void);
 int rt_abi_version(void);

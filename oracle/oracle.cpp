@@ -871,6 +871,12 @@ int orc_scene_finalize(orc_scene_t* sc) {
     return sc->s.light;
 }
 
+// Mesh::intersect without the octree (geometry.rs:886-903, `octree: None`: brute-force nearest
+// triangle, strict <) for every mesh of the scene when accel == 0; the octree walk again when 1.
+void orc_scene_set_mesh_accel(orc_scene_t* sc, int accel) {
+    for (Mesh& m : sc->s.meshes) m.accelerated = accel != 0;
+}
+
 // Octree shape: out[0]=nodes, out[1]=parents, out[2]=leaves, out[3]=tri refs, out[4]=max leaf size, out[5]=max leaf depth
 int orc_mesh_stats(orc_scene_t* sc, int obj, int64_t out[6], double bbox[6], double* surface_area, int64_t* ntris, int64_t* nverts) {
     const Object& o = sc->s.objects[obj];

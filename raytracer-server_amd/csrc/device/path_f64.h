@@ -623,6 +623,53 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
     return WALK_RUN;
 }
 
+// Mesh::intersect's `octree: None` branch (geometry.rs:886-903): the nearest triangle hit, strict <
+// in triangle order (ties go to the lower index), found through the mesh's BVH: near child first
+// (by the ray's direction along the split axis), far child on a per-lane stack in LDS. Boxes are
+// culled with the padded slab test against the best t so far, so a triangle that could win is
+// never skipped; the tie rule makes the result independent of the visiting order. tmax: a hit
+// beyond it cannot be used by the caller (closest other object / shadow distance); hits at exactly
+// tmax are kept (the caller's tie rule decides). Blocks of 256 threads.
+__shared__ int32_t s_bvh_stack[kBvhMaxDepth * 256];
+RT_DEV bool mesh_hit_bvh(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax,
+                         double* t, int* prim) {
+    typedef __attribute__((address_space(3))) int32_t LdsI32;
+    LdsI32* stk = (LdsI32*)s_bvh_stack + threadIdx.x;  // entry k at [k * 256]
+    double bt = tmax;
+    int best = -1;
+    if (m.bvh_n <= 0) return false;
+    int i = m.bvh_base, sp = 0;
+    for (;;) {
+        const DevBvhNode& nd = sc.bvh[i];
+        const double bx[6] = {nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2]};
+        if (near_box(bx, ray, inv, m.cull_pad, bt)) {
+            if (nd.count == 0) {
+                const double dk = nd.axis == 0 ? ray.d.x : nd.axis == 1 ? ray.d.y : ray.d.z;
+                const int l = i + 1, r = nd.a;
+                stk[sp * 256] = dk < 0. ? l : r;  // far child
+                ++sp;
+                i = dk < 0. ? r : l;
+                continue;
+            }
+            for (int k = 0; k < nd.count; ++k) {
+                double tt;
+                const int id = sc.btri_id[nd.a + k];
+                if (tri_t(sc.btris[nd.a + k], ray, &tt) && (tt < bt || (tt == bt && (best < 0 || id < best)))) {
+                    bt = tt;
+                    best = id;
+                }
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        i = stk[sp * 256];
+    }
+    if (best < 0) return false;
+    *t = bt;
+    *prim = best;
+    return true;
+}
+
 // Whole traversal in one call (megakernel / trace kernel).
 RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax, double* t,
                      int* prim) {
@@ -642,6 +689,7 @@ struct Cfg {
     static constexpr bool phong = (F & 2) != 0;  // scene has a Phong BRDF
     static constexpr bool mis = (F & 4) != 0;    // RT_FLAG_MIS
     static constexpr bool compact = (F & 8) != 0;  // scene fits the compact tables (DevScene)
+    static constexpr bool bvh = (F & 16) != 0;     // RT_FLAG_MESH_NEAREST: nearest-triangle meshes via the BVH
 };
 
 // Per-call view of the compact tables (scene_layout.h: CompactTab). The empty asm makes the pointer
@@ -659,7 +707,8 @@ RT_DEV bool object_t(const DevScene& sc, const DevObject& o, const Ray& ray, con
                      double tmax = INFINITY) {
     if (o.geom == GEOM_SPHERE) return sphere_t(o, ray, t);
     if (o.geom == GEOM_PLANE) return plane_t(o, ray, inv, t);
-    if constexpr (C::mesh) return mesh_hit(sc, sc.meshes[o.mesh], ray, inv, tmax, t, prim);
+    if constexpr (C::mesh && C::bvh) return mesh_hit_bvh(sc, sc.meshes[o.mesh], ray, inv, tmax, t, prim);
+    if constexpr (C::mesh && !C::bvh) return mesh_hit(sc, sc.meshes[o.mesh], ray, inv, tmax, t, prim);
     return false;
 }
 

@@ -39,12 +39,21 @@ struct alignas(16) DevObject {
 // All indices are GLOBAL (mesh bases already added).
 struct alignas(16) DevMesh {
     int32_t node_base, n_nodes, root_leaf, max_depth;  // root_leaf: leaf id when the root is a leaf, else -1
-    int32_t tri_base, n_tris, pad0, pad1;
+    int32_t tri_base, n_tris, bvh_base, bvh_n;  // bvh: this mesh's nodes in DevScene::bvh
     double root_box[6];       // Octree.bounding_box (min xyz, max xyz)
     double oct_center[8][3];  // centres of the ROOT box's octants: traversal order key (geometry.rs:1249-1260)
     double surface_area;      // Mesh.surface_area (mesh-light pdf, geometry.rs:591)
     double total_weight;      // sum of triangle areas (WeightedIndex total)
     double cull_pad;          // near_box padding: 1e-7 * max(1, |box coordinates|)
+};
+
+// BVH over a mesh's triangles for the nearest-triangle mode (RT_FLAG_MESH_NEAREST), nodes in DFS
+// pre-order: an inner node's left child is the next node, `a` its right child, `axis` the split
+// axis (left = smaller centroids); a leaf (count > 0) holds btris[a .. a + count).
+constexpr int kBvhMaxDepth = 32;  // the traversal's per-lane stack (LDS)
+struct alignas(16) DevBvhNode {
+    double bmin[3], bmax[3];
+    int32_t a, count, axis, pad;
 };
 
 // node_kids[node][8] entries: -1 empty octant, >= 0 parent node, <= -2 leaf id (-2 - entry).
@@ -93,6 +102,9 @@ struct DevScene {
     const DevTri* tris;         // per triangle (surface normal, mesh-light sampling)
     const double* tri_cum_area;  // per triangle, cumulative area within its mesh (mesh-light pick)
     const CompactTab* ctab;     // compact tables (valid when `compact`; see Cfg::compact)
+    const DevBvhNode* bvh;      // nearest-triangle mode: BVH nodes (DevMesh::bvh_base)
+    const DevTri* btris;        // BVH leaf triangles, in leaf order
+    const int32_t* btri_id;     // [btri] global triangle index
     int32_t n_objects, light, n_meshes, compact;
     double cam_pos[3], cam_dir[3];
     double light_pdf;           // area pdf of the light: 1 / (4 pi r^2) (geometry.rs:583) or

@@ -12,7 +12,7 @@ struct RenderArgs {
     int32_t width, height, x0, y0, tw, th;
     int32_t n_samples;  // spp / 4 per subpixel
     int32_t mis;
-    int32_t features;  // Cfg<F> bits: 1 mesh, 2 phong, 4 mis (kernel specialisation)
+    int32_t features;  // Cfg<F> bits: 1 mesh, 2 phong, 4 mis, 8 compact, 16 nearest-triangle meshes (BVH)
     int32_t mesh_nodes;  // octree nodes of the largest mesh (megakernel choice)
     int32_t row_step;    // tile row i = screen row y0 + i * row_step
     int32_t tail_cps;    // split tail: chunks per subpixel
@@ -35,6 +35,6 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double
                                  double* tail_buf, size_t tail_cap, hipStream_t st);
 hipError_t launch_finalize_f64(const RenderArgs& a, const double* sub_buf, hipStream_t st);
 hipError_t launch_trace_f64(const DevScene& sc, long n, const double* o, const double* d, double* t, int32_t* obj,
-                            double* pos, double* nrm, hipStream_t st);
+                            double* pos, double* nrm, bool mesh_nearest, hipStream_t st);
 
 }  // namespace rt

@@ -521,11 +521,12 @@ __global__ __launch_bounds__(256) void k_finalize_f64(RenderArgs a, const double
 
 __global__ __launch_bounds__(256) void k_trace_f64(DevScene sc, long n, const double* __restrict__ o,
                                                    const double* __restrict__ d, double* t, int32_t* obj,
-                                                   double* pos, double* nrm) {
+                                                   double* pos, double* nrm, int nearest) {
     long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Ray r{v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2])};
-    HitRec h = sc.compact ? trace_closest<Cfg<9>>(sc, r) : trace_closest<Cfg<1>>(sc, r);
+    HitRec h = nearest ? (sc.compact ? trace_closest<Cfg<25>>(sc, r) : trace_closest<Cfg<17>>(sc, r))
+                       : (sc.compact ? trace_closest<Cfg<9>>(sc, r) : trace_closest<Cfg<1>>(sc, r));
     obj[i] = h.obj;
     t[i] = h.obj >= 0 ? h.t : 0.0;
     if (h.obj >= 0) {
@@ -631,6 +632,19 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, dou
     // camera-sample buffer refill threshold (lanes per wave; 0 disables the buffer)
     static const int refill = env_int("RT_MK_CAM_REFILL", 24);
     static const int wmin = std::max(1, env_int("RT_MK_WALK_MIN", 1));
+    if (a.features & 16) {
+        // nearest-triangle meshes (RT_FLAG_MESH_NEAREST): BVH traversal inline, 3 waves/SIMD
+#define RT_MB_CASE(F)                                                                             \
+    case F:                                                                                       \
+        launch_mk<F, 3>(sc, a, sub_buf, next_sub, nsub, refill, tail_buf, tail_cap, st);          \
+        break;
+        switch (a.features & 31) {
+            RT_MB_CASE(17) RT_MB_CASE(19) RT_MB_CASE(21) RT_MB_CASE(23) RT_MB_CASE(25) RT_MB_CASE(27) RT_MB_CASE(29)
+            RT_MB_CASE(31)
+        }
+#undef RT_MB_CASE
+        return hipGetLastError();
+    }
     if (interleave && (a.features & 9) == 9 && a.mesh_nodes >= interleave) {
 #define RT_MM_CASE(F)                                                        \
     case F:                                                                  \
@@ -727,10 +741,11 @@ extern "C" int rt_debug_counters(unsigned long long out[16]) {
 }
 
 hipError_t launch_trace_f64(const DevScene& sc, long n, const double* o, const double* d, double* t, int32_t* obj,
-                            double* pos, double* nrm, hipStream_t st) {
+                            double* pos, double* nrm, bool mesh_nearest, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     long blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(k_trace_f64, dim3((unsigned)blocks), dim3(256), 0, st, sc, n, o, d, t, obj, pos, nrm);
+    hipLaunchKernelGGL(k_trace_f64, dim3((unsigned)blocks), dim3(256), 0, st, sc, n, o, d, t, obj, pos, nrm,
+                       mesh_nearest ? 1 : 0);
     return hipGetLastError();
 }
 

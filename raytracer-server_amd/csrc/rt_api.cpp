@@ -1,6 +1,7 @@
 // C ABI (include/rt_ffi.h): scene packing + per-device upload, render dispatch, error reporting.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -45,6 +46,9 @@ struct Packed {
     std::vector<int32_t> ltri_id;
     std::vector<rt::DevTri> tris;
     std::vector<double> cum_area;
+    std::vector<rt::DevBvhNode> bvh;  // nearest-triangle mode (RT_FLAG_MESH_NEAREST)
+    std::vector<rt::DevTri> btris;
+    std::vector<int32_t> btri_id;
 };
 
 struct DeviceCopy {
@@ -74,6 +78,74 @@ void cp3(double* dst, const rt::host::D3& v) {
     dst[0] = v.x;
     dst[1] = v.y;
     dst[2] = v.z;
+}
+
+// BVH over one mesh's triangles for the nearest-triangle mode: median split of the triangle
+// centroids along the longest axis, leaves of <= 4 triangles (or at depth kBvhMaxDepth - 1), nodes
+// in DFS pre-order (DevBvhNode). Node boxes are the triangles' vertex bounds; the traversal's slab test pads
+// them (near_box, DevMesh::cull_pad), so a triangle the ray hits is never culled.
+void build_bvh(Packed& p, const rt::host::Mesh& m, int32_t tri_base) {
+    using rt::host::D3;
+    struct Item { double lo[3], hi[3], c[3]; int32_t id; };
+    const size_t n = m.num_triangles();
+    std::vector<Item> it(n);
+    for (size_t t = 0; t < n; ++t) {
+        const D3 v[3] = {m.vertices[m.indices[3 * t]], m.vertices[m.indices[3 * t + 1]], m.vertices[m.indices[3 * t + 2]]};
+        Item& x = it[t];
+        x.id = (int32_t)t;
+        for (int k = 0; k < 3; ++k) {
+            const double a = k == 0 ? v[0].x : k == 1 ? v[0].y : v[0].z;
+            const double b = k == 0 ? v[1].x : k == 1 ? v[1].y : v[1].z;
+            const double c = k == 0 ? v[2].x : k == 1 ? v[2].y : v[2].z;
+            x.lo[k] = std::min({a, b, c});
+            x.hi[k] = std::max({a, b, c});
+            x.c[k] = 0.5 * (x.lo[k] + x.hi[k]);
+        }
+    }
+    struct Rec {
+        Packed& p;
+        std::vector<Item>& it;
+        int32_t tri_base;
+        void build(size_t b, size_t e, int depth) {
+            const size_t node = p.bvh.size();
+            p.bvh.push_back(rt::DevBvhNode{});
+            rt::DevBvhNode nd{};
+            double clo[3], chi[3];
+            for (int k = 0; k < 3; ++k) {
+                nd.bmin[k] = clo[k] = INFINITY;
+                nd.bmax[k] = chi[k] = -INFINITY;
+            }
+            for (size_t i = b; i < e; ++i)
+                for (int k = 0; k < 3; ++k) {
+                    nd.bmin[k] = std::min(nd.bmin[k], it[i].lo[k]);
+                    nd.bmax[k] = std::max(nd.bmax[k], it[i].hi[k]);
+                    clo[k] = std::min(clo[k], it[i].c[k]);
+                    chi[k] = std::max(chi[k], it[i].c[k]);
+                }
+            if (e - b <= 4 || depth + 1 >= rt::kBvhMaxDepth) {
+                nd.a = (int32_t)p.btris.size();
+                nd.count = (int32_t)(e - b);
+                std::sort(it.begin() + b, it.begin() + e, [](const Item& x, const Item& y) { return x.id < y.id; });
+                for (size_t i = b; i < e; ++i) {
+                    p.btris.push_back(p.tris[tri_base + it[i].id]);
+                    p.btri_id.push_back(tri_base + it[i].id);
+                }
+            } else {
+                int ax = 0;
+                for (int k = 1; k < 3; ++k)
+                    if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
+                const size_t mid = (b + e) / 2;
+                std::nth_element(it.begin() + b, it.begin() + mid, it.begin() + e,
+                                 [ax](const Item& x, const Item& y) { return x.c[ax] < y.c[ax] || (x.c[ax] == y.c[ax] && x.id < y.id); });
+                nd.axis = ax;
+                build(b, mid, depth + 1);
+                nd.a = (int32_t)p.bvh.size();  // global index of the right child
+                build(mid, e, depth + 1);
+            }
+            p.bvh[node] = nd;
+        }
+    } rec{p, it, tri_base};
+    if (n > 0) rec.build(0, n, 0);
 }
 
 void pack_scene(rt_scene* s) {
@@ -138,6 +210,9 @@ void pack_scene(rt_scene* s) {
             }
         }
         if (oc.size() > 0 && oc.kind[0]) dm.root_leaf = leaf_of[0];
+        dm.bvh_base = (int32_t)p.bvh.size();
+        build_bvh(p, m, dm.tri_base);
+        dm.bvh_n = (int32_t)p.bvh.size() - dm.bvh_base;
         for (size_t i = 0; i < oc.size(); ++i) {
             p.up.push_back(int2{oc.parent[i] >= 0 ? oc.parent[i] + dm.node_base : -1, oc.slot[i]});
             for (int k = 0; k < 8; ++k) {
@@ -226,7 +301,7 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
     if (!dc.ready) {
         const Packed& p = s->packed;
         std::vector<char> blob;
-        size_t o_obj, o_mesh, o_kids, o_up, o_leaf, o_ltri, o_lid, o_tris, o_cum, o_tab;
+        size_t o_obj, o_mesh, o_kids, o_up, o_leaf, o_ltri, o_lid, o_tris, o_cum, o_tab, o_bvh, o_btri, o_bid;
         std::vector<rt::CompactTab> tab(1);
         std::memset(tab.data(), 0, sizeof(rt::CompactTab));
         int32_t compact = 0;
@@ -241,6 +316,9 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         put(blob, &o_lid, p.ltri_id);
         put(blob, &o_tris, p.tris);
         put(blob, &o_cum, p.cum_area);
+        put(blob, &o_bvh, p.bvh);
+        put(blob, &o_btri, p.btris);
+        put(blob, &o_bid, p.btri_id);
         void* d = nullptr;
         HIP_TRY(hipMalloc(&d, blob.size()));
         hipError_t e = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice);
@@ -261,6 +339,9 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.tri_cum_area = (const double*)(b + o_cum);
         ds.n_objects = (int32_t)p.objects.size();
         ds.ctab = (const rt::CompactTab*)(b + o_tab);
+        ds.bvh = (const rt::DevBvhNode*)(b + o_bvh);
+        ds.btris = (const rt::DevTri*)(b + o_btri);
+        ds.btri_id = (const int32_t*)(b + o_bid);
         ds.compact = compact;
         ds.light = s->host.light;
         ds.light_pdf = 0.0;
@@ -334,6 +415,7 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
         bool phong = false;
         for (const auto& o : s->host.objects) phong |= o.brdf == RT_BRDF_PHONG;
         a.features = (s->host.meshes.empty() ? 0 : 1) | (phong ? 2 : 0) | (a.mis ? 4 : 0) | (ds.compact ? 8 : 0);
+        if ((p->flags & RT_FLAG_MESH_NEAREST) && !s->host.meshes.empty()) a.features |= 16;
         for (const auto& m : s->host.meshes) a.mesh_nodes = std::max(a.mesh_nodes, (int32_t)m.octree.size());
     }
     a.seed = p->seed;
@@ -342,6 +424,8 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
     a.sub_out = d_sub;
     a.rgb_out = d_rgb;
     if (p->flags & RT_FLAG_FP32) return fail(RT_E_INVAL, "RT_FLAG_FP32 is not available in this build");
+    if ((p->flags & RT_FLAG_MESH_NEAREST) && !(p->flags & RT_FLAG_MEGAKERNEL))
+        return fail(RT_E_INVAL, "RT_FLAG_MESH_NEAREST needs RT_FLAG_MEGAKERNEL");
     std::unique_ptr<rt::Workspace> ws = take_workspace(s, p->device);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (stats) {
@@ -569,6 +653,11 @@ int rt_render(const rt_scene* scene, const rt_render_params* p, uint8_t* rgb_out
 
 int rt_trace_rays(const rt_scene* scene, int32_t device, int64_t n, const double* origins, const double* dirs, double* t,
                   int32_t* object, double* pos, double* normal) {
+    return rt_trace_rays_flags(scene, device, 0u, n, origins, dirs, t, object, pos, normal);
+}
+
+int rt_trace_rays_flags(const rt_scene* scene, int32_t device, uint32_t flags, int64_t n, const double* origins,
+                        const double* dirs, double* t, int32_t* object, double* pos, double* normal) {
     if (!scene || n < 0 || (n && (!origins || !dirs || !t || !object))) return fail(RT_E_INVAL, "null argument");
     if (n == 0) return RT_OK;
     HIP_TRY(hipSetDevice(device));
@@ -587,7 +676,8 @@ int rt_trace_rays(const rt_scene* scene, int32_t device, int64_t n, const double
     int32_t* d_id = (int32_t*)(buf + 4 * v3 + (size_t)n * sizeof(double));
     hipError_t e = hipMemcpy(d_o, origins, v3, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d_d, dirs, v3, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = rt::launch_trace_f64(ds, (long)n, d_o, d_d, d_t, d_id, d_pos, d_n, nullptr);
+    if (e == hipSuccess)
+        e = rt::launch_trace_f64(ds, (long)n, d_o, d_d, d_t, d_id, d_pos, d_n, (flags & RT_FLAG_MESH_NEAREST) != 0, nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(t, d_t, (size_t)n * sizeof(double), hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipMemcpy(object, d_id, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost);

@@ -24,6 +24,7 @@ RT_CANCELLED = 1
 FLAG_MIS = 1 << 0
 FLAG_MEGAKERNEL = 1 << 1
 FLAG_FP32 = 1 << 2
+FLAG_MESH_NEAREST = 1 << 3  # Mesh::intersect without the octree (geometry.rs:886-903), BVH on the device
 
 BRDF_DIFFUSE, BRDF_SPECULAR, BRDF_PHONG = 0, 1, 2
 GEOM_SPHERE, GEOM_PLANE, GEOM_MESH = 0, 1, 2
@@ -69,7 +70,7 @@ class SceneDesc(ctypes.Structure):
 
 
 _EXPORTS = ["rt_scene_load_toml", "rt_scene_create", "rt_scene_destroy", "rt_scene_info", "rt_scene_mesh",
-            "rt_render", "rt_render_device", "rt_trace_rays", "rt_last_error", "rt_abi_version",
+            "rt_render", "rt_render_device", "rt_trace_rays", "rt_trace_rays_flags", "rt_last_error", "rt_abi_version",
             "rt_device_count"]
 
 
@@ -92,6 +93,9 @@ def _load():
     L.rt_render_device.argtypes = [vp, P(RenderParams), vp, vp, vp, P(RenderStats)]
     L.rt_trace_rays.argtypes = [vp, ctypes.c_int32, ctypes.c_int64, P(ctypes.c_double), P(ctypes.c_double),
                                 P(ctypes.c_double), P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_double)]
+    L.rt_trace_rays_flags.argtypes = [vp, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int64, P(ctypes.c_double),
+                                      P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_int32), P(ctypes.c_double),
+                                      P(ctypes.c_double)]
     L.rt_last_error.restype = ctypes.c_char_p
     L.rt_last_error.argtypes = []
     L.rt_abi_version.argtypes = []
@@ -220,7 +224,7 @@ class Scene:
         return dict(bbox=bbox, surface_area=sa.value, vertices=verts, indices=idx, kind=kind, child=child,
                     leaf_off=off, leaf_cnt=cnt, refs=refs[:nr])
 
-    def trace_ray(self, origins, dirs, device=0):
+    def trace_ray(self, origins, dirs, device=0, mesh_nearest=False):
         o = np.ascontiguousarray(origins, dtype=np.float64).reshape(-1, 3)
         d = np.ascontiguousarray(dirs, dtype=np.float64).reshape(-1, 3)
         n = o.shape[0]
@@ -229,8 +233,8 @@ class Scene:
         pos = np.zeros((n, 3))
         nrm = np.zeros((n, 3))
         D = ctypes.c_double
-        _check(lib.rt_trace_rays(self._h, device, n, _ptr(o, D), _ptr(d, D), _ptr(t, D), _ptr(ids, ctypes.c_int32),
-                                 _ptr(pos, D), _ptr(nrm, D)))
+        _check(lib.rt_trace_rays_flags(self._h, device, FLAG_MESH_NEAREST if mesh_nearest else 0, n, _ptr(o, D),
+                                       _ptr(d, D), _ptr(t, D), _ptr(ids, ctypes.c_int32), _ptr(pos, D), _ptr(nrm, D)))
         return t, ids, pos, nrm
 
 
@@ -241,9 +245,10 @@ def make_params(width, height, spp, seed=0x5EED, tile=None, flags=0, device=0, r
 
 
 def render(scene, width, height, spp, seed=0x5EED, tile=None, mis=False, megakernel=False, device=0,
-           want_sub=False, cancel=None, row_step=1):
-    """Renders a tile to host memory. Returns (rgb[th, tw, 3] u8, sub[th, tw, 4, 3] f64 or None, stats)."""
-    flags = (FLAG_MIS if mis else 0) | (FLAG_MEGAKERNEL if megakernel else 0)
+           want_sub=False, cancel=None, row_step=1, mesh_nearest=False):
+    """Renders a tile to host memory. Returns (rgb[th, tw, 3] u8, sub[th, tw, 4, 3] f64 or None, stats).
+    mesh_nearest: Mesh::intersect's `octree: None` semantics (RT_FLAG_MESH_NEAREST, megakernel only)."""
+    flags = (FLAG_MIS if mis else 0) | (FLAG_MEGAKERNEL if megakernel else 0) | (FLAG_MESH_NEAREST if mesh_nearest else 0)
     p = make_params(width, height, spp, seed, tile, flags, device, row_step)
     rgb = np.zeros((p.tile_h, p.tile_w, 3), dtype=np.uint8)
     sub = np.zeros((p.tile_h, p.tile_w, 4, 3), dtype=np.float64) if want_sub else None

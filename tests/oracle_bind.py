@@ -57,6 +57,8 @@ def lib():
         L.orc_draws.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                 ctypes.c_int, _D]
         L.orc_trace.argtypes = [ctypes.c_void_p, ctypes.c_int64, _D, _D, _D, _I32, _D, _D]
+        L.orc_scene_set_mesh_accel.restype = None
+        L.orc_scene_set_mesh_accel.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.orc_render.restype = ctypes.c_int64
         L.orc_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
@@ -82,7 +84,7 @@ _TF = {"translate": 0, "scale": 1, "rotate_x": 2, "rotate_y": 3, "rotate_z": 4}
 class OracleScene:
     """Scene built by the oracle from a reference scene TOML (scene.rs:357 SceneSpec::to_scene)."""
 
-    def __init__(self, toml_path, assets_dir=None):
+    def __init__(self, toml_path, assets_dir=None, mesh_nearest=False):
         import tomli
 
         with open(toml_path, "rb") as f:
@@ -144,6 +146,8 @@ class OracleScene:
         self.light = L.orc_scene_finalize(self.h)
         if self.light < 0:
             raise RuntimeError(L.orc_scene_error(self.h).decode())
+        if mesh_nearest:  # Mesh::intersect's `octree: None` branch (geometry.rs:886-903)
+            L.orc_scene_set_mesh_accel(self.h, 0)
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:

@@ -86,6 +86,39 @@ def test_render_parity_small(name, megakernel, rt, gpu_scenes, oracle_scenes):
     _assert_parity(rgb_g, sub_g, rgb_o, sub_o, f"{name}/{'mk' if megakernel else 'wf'}")
 
 
+@pytest.fixture(scope="module")
+def oracle_nearest(oracle):
+    """Oracle scenes whose meshes take Mesh::intersect's `octree: None` branch (geometry.rs:886-903)."""
+    return {n: oracle.OracleScene(scene_path(n), mesh_nearest=True) for n in ("cubes", "flying_unicorn")}
+
+
+@pytest.mark.parametrize("name", ["cubes", "flying_unicorn"])
+def test_trace_mesh_nearest_bit_exact(name, gpu_scenes, oracle_nearest, oracle_scenes):
+    """RT_FLAG_MESH_NEAREST: the device BVH returns the brute-force nearest triangle (strict <,
+    ties to the lower index) — the same hits as the oracle's loop over every triangle, bit for bit."""
+    rng = np.random.default_rng(4321)
+    o, d = _rays_for(name, 30000 if name == "cubes" else 6000, rng)  # the oracle tests every triangle
+    t_g, id_g, p_g, n_g = gpu_scenes[name].trace_ray(o, d, mesh_nearest=True)
+    t_o, id_o, p_o, n_o = oracle_nearest[name].trace(o, d)
+    exact = (id_g == id_o) & (t_g == t_o) & np.all(p_g == p_o, axis=1) & np.all(n_g == n_o, axis=1)
+    assert exact.all(), f"{name}: {np.count_nonzero(~exact)} of {len(exact)} hits differ"
+    # the two mesh semantics differ on some rays of the non-convex unicorn (the octree returns the
+    # first subtree with a hit); on the convex cubes they coincide
+    t_oct, id_oct, _, _ = oracle_scenes[name].trace(o, d)
+    assert (np.count_nonzero(t_oct != t_o) > 0) == (name == "flying_unicorn")
+
+
+@pytest.mark.parametrize("name", ["cubes", "flying_unicorn"])
+def test_render_parity_mesh_nearest(name, rt, gpu_scenes, oracle_nearest):
+    w, h, spp = (96, 72, 16) if name == "cubes" else (24, 18, 4)  # oracle: every triangle per mesh query
+    rgb_g, sub_g, st = rt.render(gpu_scenes[name], w, h, spp, SEED, megakernel=True, mesh_nearest=True, want_sub=True)
+    rgb_o, sub_o, st_o = oracle_nearest[name].render(w, h, spp, SEED)
+    assert 0.9 * st_o["vertices"] <= st["vertices"] <= st_o["vertices"]
+    _assert_parity(rgb_g, sub_g, rgb_o, sub_o, f"{name}/nearest")
+    with pytest.raises(rt.RtError):  # megakernel only
+        rt.render(gpu_scenes[name], 8, 8, 4, SEED, megakernel=False, mesh_nearest=True)
+
+
 def test_megakernel_equals_wavefront(rt, gpu_scenes):
     for name in ("cornell_box", "flying_unicorn"):
         a = rt.render(gpu_scenes[name], 128, 96, 8, SEED, want_sub=True, megakernel=True)

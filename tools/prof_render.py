@@ -1,4 +1,4 @@
-"""One render through the C ABI for profiling runs: python tools/prof_render.py SCENE W H SPP [mk|wf] [mis]"""
+"""One render through the C ABI for profiling runs: python tools/prof_render.py SCENE W H SPP [mk|wf] [mis] [nearest]"""
 import os
 import sys
 import time
@@ -9,12 +9,13 @@ import rt_amd  # noqa: E402
 
 scene, w, h, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
 mode = sys.argv[5] if len(sys.argv) > 5 else "mk"
-mis = len(sys.argv) > 6 and sys.argv[6] == "mis"
+mis = "mis" in sys.argv[6:]
+nearest = "nearest" in sys.argv[6:]  # RT_FLAG_MESH_NEAREST (BVH)
 s = rt_amd.Scene.from_toml(os.path.join(REPO, "scenes", f"{scene}.toml"))
 t = time.perf_counter()
-rgb, _, st = rt_amd.render(s, w, h, spp, megakernel=(mode == "mk"), mis=mis)
+rgb, _, st = rt_amd.render(s, w, h, spp, megakernel=(mode == "mk"), mis=mis, mesh_nearest=nearest)
 dt = time.perf_counter() - t
 n = w * h * 4 * (spp // 4)
-print(f"{scene} {w}x{h}x{spp} {mode}{' mis' if mis else ''}: {dt*1e3:.1f} ms wall, {st['device_ms']:.1f} ms device, "
+print(f"{scene} {w}x{h}x{spp} {mode}{' mis' if mis else ''}{' nearest' if nearest else ''}: {dt*1e3:.1f} ms wall, {st['device_ms']:.1f} ms device, "
       f"{n / st['device_ms'] / 1e3:.1f} Msamples/s, {st['vertices'] / max(1, n):.3f} vertices/sample, "
       f"iterations {st['iterations']}, rgb sha1 {__import__('hashlib').sha1(rgb.tobytes()).hexdigest()[:12]}")
