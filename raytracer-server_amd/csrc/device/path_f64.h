@@ -629,44 +629,68 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
 // culled with the padded slab test against the best t so far, so a triangle that could win is
 // never skipped; the tie rule makes the result independent of the visiting order. tmax: a hit
 // beyond it cannot be used by the caller (closest other object / shadow distance); hits at exactly
-// tmax are kept (the caller's tie rule decides). Blocks of 256 threads.
-__shared__ int32_t s_bvh_stack[kBvhMaxDepth * 256];
-RT_DEV bool mesh_hit_bvh(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax,
-                         double* t, int* prim) {
-    typedef __attribute__((address_space(3))) int32_t LdsI32;
-    LdsI32* stk = (LdsI32*)s_bvh_stack + threadIdx.x;  // entry k at [k * 256]
-    double bt = tmax;
-    int best = -1;
-    if (m.bvh_n <= 0) return false;
-    int i = m.bvh_base, sp = 0;
-    for (;;) {
-        const DevBvhNode& nd = sc.bvh[i];
-        const double bx[6] = {nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2]};
-        if (near_box(bx, ray, inv, m.cull_pad, bt)) {
-            if (nd.count == 0) {
-                const double dk = nd.axis == 0 ? ray.d.x : nd.axis == 1 ? ray.d.y : ray.d.z;
-                const int l = i + 1, r = nd.a;
-                stk[sp * 256] = dk < 0. ? l : r;  // far child
-                ++sp;
-                i = dk < 0. ? r : l;
-                continue;
-            }
-            for (int k = 0; k < nd.count; ++k) {
-                double tt;
-                const int id = sc.btri_id[nd.a + k];
-                if (tri_t(sc.btris[nd.a + k], ray, &tt) && (tt < bt || (tt == bt && (best < 0 || id < best)))) {
-                    bt = tt;
-                    best = id;
-                }
+// tmax are kept (the caller's tie rule decides).
+// bvh_step does one node per call (resumable, for the interleaved mesh kernel): WALK_RUN, or
+// WALK_HIT with the nearest triangle in w.bt / w.best, or WALK_MISS. With shadow_dist >= 0 it
+// returns as soon as a triangle blocks the shadow ray (t + 0.001 < dist, mutually_visible).
+struct BvhWalk {
+    int32_t cur, sp, best;
+    double bt;
+};
+RT_DEV void bvh_begin(const DevMesh& m, double tmax, BvhWalk& w) {
+    w.cur = m.bvh_base;
+    w.sp = 0;
+    w.best = -1;
+    w.bt = tmax;
+}
+template <class Stack>
+RT_DEV int bvh_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, BvhWalk& w,
+                    const Stack& stk, double shadow_dist) {
+    const DevBvhNode& nd = sc.bvh[w.cur];
+    const double bx[6] = {nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2]};
+    if (near_box(bx, ray, inv, m.cull_pad, w.bt)) {
+        if (nd.count == 0) {
+            const double dk = nd.axis == 0 ? ray.d.x : nd.axis == 1 ? ray.d.y : ray.d.z;
+            const int l = w.cur + 1, r = nd.a;
+            stk.at(w.sp) = dk < 0. ? l : r;  // far child
+            ++w.sp;
+            w.cur = dk < 0. ? r : l;
+            return 0;  // WALK_RUN
+        }
+        for (int k = 0; k < nd.count; ++k) {
+            double tt;
+            const int id = sc.btri_id[nd.a + k];
+            if (tri_t(sc.btris[nd.a + k], ray, &tt) && (tt < w.bt || (tt == w.bt && (w.best < 0 || id < w.best)))) {
+                w.bt = tt;
+                w.best = id;
             }
         }
-        if (sp == 0) break;
-        --sp;
-        i = stk[sp * 256];
+        if (shadow_dist >= 0. && w.best >= 0 && !(w.bt + 0.001 >= shadow_dist)) return 1;  // blocked
     }
-    if (best < 0) return false;
-    *t = bt;
-    *prim = best;
+    if (w.sp == 0) return w.best >= 0 ? 1 : 2;  // WALK_HIT / WALK_MISS
+    --w.sp;
+    w.cur = stk.at(w.sp);
+    return 0;
+}
+// Fused traversal (analytic megakernel, trace kernel): the stack in its own LDS array.
+__shared__ int32_t s_bvh_stack[kBvhMaxDepth * 256];  // blocks of 256 threads
+struct BvhLdsStack {
+    typedef __attribute__((address_space(3))) int32_t LdsI32;
+    LdsI32* p;
+    RT_DEV LdsI32& at(int e) const { return p[e * 256]; }
+};
+RT_DEV bool mesh_hit_bvh(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax,
+                         double* t, int* prim) {
+    if (m.bvh_n <= 0) return false;
+    const BvhLdsStack stk{(BvhLdsStack::LdsI32*)s_bvh_stack + threadIdx.x};
+    BvhWalk w;
+    bvh_begin(m, tmax, w);
+    int st;
+    while ((st = bvh_step(sc, m, ray, inv, w, stk, -1.0)) == 0) {
+    }
+    if (st != 1) return false;
+    *t = w.bt;
+    *prim = w.best;
     return true;
 }
 

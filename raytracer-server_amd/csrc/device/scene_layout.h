@@ -50,7 +50,7 @@ struct alignas(16) DevMesh {
 // BVH over a mesh's triangles for the nearest-triangle mode (RT_FLAG_MESH_NEAREST), nodes in DFS
 // pre-order: an inner node's left child is the next node, `a` its right child, `axis` the split
 // axis (left = smaller centroids); a leaf (count > 0) holds btris[a .. a + count).
-constexpr int kBvhMaxDepth = 32;  // the traversal's per-lane stack (LDS)
+constexpr int kBvhMaxDepth = 20;  // the traversal's per-lane stack (LDS; 20 entries fit the mesh kernel's park)
 struct alignas(16) DevBvhNode {
     double bmin[3], bmax[3];
     int32_t a, count, axis, pad;

@@ -289,6 +289,58 @@ RT_DEV void park_load(const Park& p, WalkRegs& r) {
     r.hobj = p.I(11); r.hprim = p.I(12); r.g = p.I(13); r.mi = p.I(14); r.occluded = p.I(15);
 }
 
+// Nearest-triangle mode (Cfg::bvh): the BVH walk parks cur / sp / best / bt in the octree walk's
+// slots I(0), I(1), I(10), D(15), and its stack in the slots the octree walk would use for its
+// cursor (I(2..9)) and box (D(9..14) as int pairs): kBvhMaxDepth = 20 entries.
+struct ParkStack {
+    const Park& p;
+    RT_DEV LdsInt& at(int e) const {
+        return e < 8 ? p.I(2 + e) : ((LdsInt*)&p.D(9 + ((e - 8) >> 1)))[(e - 8) & 1];
+    }
+};
+static_assert(kBvhMaxDepth <= 8 + 12, "BVH stack does not fit the park slots");
+struct WalkRegsBvh {
+    Ray wr;
+    RayInv wi;
+    BvhWalk w;
+    double wt;
+    int32_t hobj, hprim, g, mi, occluded;
+};
+RT_DEV void park_store_bvh(const Park& p, const WalkRegsBvh& r) {
+    p.D(0) = r.wr.o.x; p.D(1) = r.wr.o.y; p.D(2) = r.wr.o.z;
+    p.D(3) = r.wr.d.x; p.D(4) = r.wr.d.y; p.D(5) = r.wr.d.z;
+    p.D(6) = r.wi.rx; p.D(7) = r.wi.ry; p.D(8) = r.wi.rz;
+    p.D(15) = r.w.bt;
+    p.D(16) = r.wt;
+    p.I(0) = r.w.cur; p.I(1) = r.w.sp; p.I(10) = r.w.best;
+    p.I(11) = r.hobj; p.I(12) = r.hprim; p.I(13) = r.g; p.I(14) = r.mi; p.I(15) = r.occluded;
+}
+RT_DEV void park_load_bvh(const Park& p, WalkRegsBvh& r) {
+    r.wr.o = v3(p.D(0), p.D(1), p.D(2));
+    r.wr.d = v3(p.D(3), p.D(4), p.D(5));
+    r.wi.rx = p.D(6); r.wi.ry = p.D(7); r.wi.rz = p.D(8);
+    r.w.bt = p.D(15);
+    r.wt = p.D(16);
+    r.w.cur = p.I(0); r.w.sp = p.I(1); r.w.best = p.I(10);
+    r.hobj = p.I(11); r.hprim = p.I(12); r.g = p.I(13); r.mi = p.I(14); r.occluded = p.I(15);
+}
+// Begins the BVH walk of the next candidate mesh after gen slot g; false when no mesh is left.
+template <class C>
+RT_DEV bool next_mesh_walk_bvh(const DevScene& sc, const Ray& r, const RayInv& inv, double tmax, int& g, int& mi,
+                               BvhWalk& w) {
+    for (++g; g < tables(sc)->n_gen; ++g) {
+        const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
+        if (o.geom != GEOM_MESH) continue;
+        const DevMesh& m = sc.meshes[o.mesh];
+        if (m.bvh_n > 0 && near_box(m.root_box, r, inv, m.cull_pad, tmax)) {
+            mi = o.mesh;
+            bvh_begin(m, tmax, w);
+            return true;
+        }
+    }
+    return false;
+}
+
 // A new walk query: ray, 1/d, query t (closest analytic hit / shadow distance) and hit so far; the
 // first walk step begins the walk of the first candidate mesh (w.cur = -1: no walk in progress).
 RT_DEV void park_query(const Park& p, const Ray& r, const RayInv& wi, double wt, int32_t hobj, int32_t hprim) {
@@ -344,7 +396,48 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     bool walking = false, cont = false;
     while (__any(active)) {
         RT_DBG_WAVE(8, lane_id_is0());
-        if (__any(walking)) {
+        if constexpr (C::bvh) {
+          if (__any(walking)) {
+            WalkRegsBvh r;
+            if (walking) park_load_bvh(park, r);
+            const ParkStack stk{park};
+            for (int k = 0; k < ksteps && (k == 0 ? __any(walking) : __popcll(__ballot(walking)) >= wmin); ++k) {
+                if (walking) {
+                    bool fin = false;
+                    if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
+                        const double tmax = phase == PH_WALK_CLOSEST ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
+                        fin = !next_mesh_walk_bvh<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w);
+                    } else {
+                        const bool shadow = phase != PH_WALK_CLOSEST;
+                        const int st = bvh_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, stk, shadow ? r.wt : -1.0);
+                        if (st != WALK_RUN) {
+                            if (!shadow) {
+                                if (st == WALK_HIT) {
+                                    HitRec h{r.wt, r.hobj, r.hprim};
+                                    consider(h, r.w.bt, tables(sc)->gen_idx[r.g], r.w.best);
+                                    r.wt = h.t;
+                                    r.hobj = h.obj;
+                                    r.hprim = h.prim;
+                                }
+                            } else {
+                                r.occluded = st == WALK_HIT && !(r.w.bt + 0.001 >= r.wt);  // mutually_visible
+                                fin = r.occluded;
+                            }
+                            r.w.cur = -1;  // next step: the next mesh, if any
+                        }
+                    }
+                    if (fin) {  // results for the vertex phase
+                        walking = false;
+                        park.D(16) = r.wt;
+                        park.I(11) = r.hobj;
+                        park.I(12) = r.hprim;
+                        park.I(15) = r.occluded;
+                    }
+                }
+            }
+            if (walking) park_store_bvh(park, r);
+          }
+        } else if (__any(walking)) {
             WalkRegs r;
             if (walking) park_load(park, r);
             // up to ksteps steps; after the first, only while at least wmin lanes still walk
@@ -632,8 +725,22 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, dou
     // camera-sample buffer refill threshold (lanes per wave; 0 disables the buffer)
     static const int refill = env_int("RT_MK_CAM_REFILL", 24);
     static const int wmin = std::max(1, env_int("RT_MK_WALK_MIN", 1));
+    static const int bvh_fused = env_int("RT_MK_BVH_FUSED", 0);  // A/B: nearest-triangle mode without interleaving
+    if (interleave && (a.features & 9) == 9 && a.mesh_nodes >= interleave && !((a.features & 16) && bvh_fused)) {
+#define RT_MM_CASE(F)                                                        \
+    case F:                                                                  \
+        launch_mm<F, 2>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, tail_buf, tail_cap, st); \
+        break;
+        switch (a.features & 31) {
+            RT_MM_CASE(9) RT_MM_CASE(11) RT_MM_CASE(13) RT_MM_CASE(15)
+            RT_MM_CASE(25) RT_MM_CASE(27) RT_MM_CASE(29) RT_MM_CASE(31)  // nearest-triangle meshes: BVH walks
+        }
+#undef RT_MM_CASE
+        return hipGetLastError();
+    }
     if (a.features & 16) {
-        // nearest-triangle meshes (RT_FLAG_MESH_NEAREST): BVH traversal inline, 3 waves/SIMD
+        // nearest-triangle meshes (RT_FLAG_MESH_NEAREST) in small or non-compact scenes: BVH
+        // traversal inline, 3 waves/SIMD
 #define RT_MB_CASE(F)                                                                             \
     case F:                                                                                       \
         launch_mk<F, 3>(sc, a, sub_buf, next_sub, nsub, refill, tail_buf, tail_cap, st);          \
@@ -643,15 +750,6 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, dou
             RT_MB_CASE(31)
         }
 #undef RT_MB_CASE
-        return hipGetLastError();
-    }
-    if (interleave && (a.features & 9) == 9 && a.mesh_nodes >= interleave) {
-#define RT_MM_CASE(F)                                                        \
-    case F:                                                                  \
-        launch_mm<F, 2>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, tail_buf, tail_cap, st); \
-        break;
-        switch (a.features & 15) { RT_MM_CASE(9) RT_MM_CASE(11) RT_MM_CASE(13) RT_MM_CASE(15) }
-#undef RT_MM_CASE
         return hipGetLastError();
     }
 #define RT_MK_CASE(F)                                                           \
