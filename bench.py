@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
     ap.add_argument("--mode", choices=["megakernel", "wavefront"], default=os.environ.get("RT_BENCH_MODE", "megakernel"))
     ap.add_argument("--mis", action="store_true")
+    ap.add_argument("--fp32", action="store_true",
+                    help="f32 perf mode (RT_FLAG_FP32, statistical parity only; not the headline f64 number)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=120)
     ap.add_argument("--cpu-spp", type=int, default=256)
@@ -135,6 +137,7 @@ def main():
     scene = rt_amd.Scene.from_toml(os.path.join(REPO, "scenes", f"{args.scene}.toml"))
     y0, th, row_step = partition(rank, world, args.height, args.partition)
     flags = (rt_amd.FLAG_MEGAKERNEL if args.mode == "megakernel" else 0) | (rt_amd.FLAG_MIS if args.mis else 0)
+    flags |= rt_amd.FLAG_FP32 if args.fp32 else 0
     params = rt_amd.make_params(args.width, args.height, args.spp, args.seed, (0, y0, args.width, th), flags, dev,
                                 row_step)
     max_rows = max(partition(r, world, args.height, args.partition)[1] for r in range(world))
@@ -196,10 +199,14 @@ def main():
         alg_bytes = BYTES_PER_SAMPLE * rank_samples + BYTES_PER_VERTEX * st["vertices"]
         achieved = alg_bytes / (dev_ms / 1e3) / 1e9
         workload = f"{args.scene} {args.width}x{args.height}x{args.spp}spp{' mis' if args.mis else ''}"
-        traffic = load_traffic(f"{workload} {args.mode}")
+        mode = args.mode + ("-f32" if args.fp32 else "")
+        kernel = "k_megakernel_f32" if args.fp32 else (
+            "k_megakernel_f64" if args.mode == "megakernel" else "k_wf_extend+k_wf_shade")
+        traffic = load_traffic(f"{workload} {mode}")
         out = {
             "metric": "Msamples/sec (pixels x spp), cornell_box 1920x1080x1024spp" if args.scene == "cornell_box"
-            and args.width == 1920 and args.height == 1080 and args.spp == 1024 else f"Msamples/sec {workload}",
+            and args.width == 1920 and args.height == 1080 and args.spp == 1024 and not args.fp32
+            else f"Msamples/sec {workload}{' (f32 perf mode)' if args.fp32 else ''}",
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -209,25 +216,25 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f32" if args.fp32 else "f64",
             "data": "synthetic: reference scene file + counter-based RNG (Philox4x32-10 -> xoroshiro128++), seed "
                     f"{args.seed:#x}",
             "config": {"workload": workload, "scene": f"scenes/{args.scene}.toml", "width": args.width,
                        "height": args.height, "spp": args.spp, "traced_spp": 4 * (args.spp // 4),
-                       "mode": args.mode, "mis": args.mis,
+                       "mode": mode, "mis": args.mis,
                        "parallelism": f"{'interleaved rows' if args.partition == 'interleave' else 'row stripes'} x{world}",
                        "frame_sha1": digest,
                        "vertices_per_sample": round(total_vertices / n_samples, 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_megakernel_f64" if args.mode == "megakernel" else "k_wf_extend+k_wf_shade",
+                         "kernel": kernel,
                          "kernel_ms": round(dev_ms, 3),
                          "alg_bytes_per_launch": alg_bytes,
                          "model": "SURVEY 8(d): 88 B/sample + 280 B/vertex (canonical f32 SoA wavefront state)"},
         }
         # The megakernel's own bound is VALU issue: PMC instructions per vertex x the
         # vertex rate of this run, against 1024 SIMDs x one wave-instruction per 4 cycles at 2.4 GHz
-        valu = load_valu(f"{args.scene} megakernel") if args.mode == "megakernel" else None
+        valu = load_valu(f"{args.scene} megakernel") if mode == "megakernel" else None
         if valu:
             rate = valu["valu_inst_per_vertex"] * st["vertices"] / (dev_ms / 1e3)
             peak = 1024 * 2.4e9 / 4

@@ -90,6 +90,25 @@ struct CompactTab {
 };
 typedef const __attribute__((address_space(4))) CompactTab CTab;
 
+// f32 perf mode (RT_FLAG_FP32, kernels/render_f32.hip): the same scene rounded to f32, statistical
+// parity only. Objects 64 B; BVH nodes 32 B with boxes rounded outward (conservative); triangles 48 B.
+struct alignas(16) Obj32 {
+    int32_t geom, brdf, mesh, emissive;
+    float emitted[3], r;
+    float k[3], r2;       // kd / ks; sphere radius squared
+    float pos[3], pad0;
+    float n[3], pad1;
+};
+struct alignas(16) Bvh32 {
+    float bmin[3];
+    int32_t a;            // right child (inner) / first btri (leaf)
+    float bmax[3];
+    int32_t cnt_axis;     // count * 4 + axis (count 0: inner node)
+};
+struct Tri32 {
+    float a[3], ab[3], ac[3], n[3];
+};
+
 struct DevScene {
     const DevObject* objects;
     const DevMesh* meshes;
@@ -105,6 +124,10 @@ struct DevScene {
     const DevBvhNode* bvh;      // nearest-triangle mode: BVH nodes (DevMesh::bvh_base)
     const DevTri* btris;        // BVH leaf triangles, in leaf order
     const int32_t* btri_id;     // [btri] global triangle index
+    const Obj32* obj32;         // f32 perf mode tables (Obj32 / Bvh32 / Tri32 above)
+    const Bvh32* bvh32;
+    const Tri32* btris32;
+    float off32;                // f32 mode: hit points are offset by off32 * n (scene-scaled epsilon)
     int32_t n_objects, light, n_meshes, compact;
     double cam_pos[3], cam_dir[3];
     double light_pdf;           // area pdf of the light: 1 / (4 pi r^2) (geometry.rs:583) or

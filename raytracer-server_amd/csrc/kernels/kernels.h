@@ -33,6 +33,9 @@ struct RenderArgs {
 // tail_buf / tail_cap: scratch for the split tail (bytes); the launcher sizes the tail to fit it.
 hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
                                  double* tail_buf, size_t tail_cap, hipStream_t st);
+// f32 perf mode (render_f32.hip): writes the subpixel means to sub_buf like the f64 megakernel.
+hipError_t launch_megakernel_f32(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
+                                 hipStream_t st);
 hipError_t launch_finalize_f64(const RenderArgs& a, const double* sub_buf, hipStream_t st);
 hipError_t launch_trace_f64(const DevScene& sc, long n, const double* o, const double* d, double* t, int32_t* obj,
                             double* pos, double* nrm, bool mesh_nearest, hipStream_t st);

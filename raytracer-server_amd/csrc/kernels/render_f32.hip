@@ -1,0 +1,421 @@
+// f32 perf mode (RT_FLAG_FP32) for gfx950: the per-pixel sample loop of server.rs:320-364 and the
+// estimator of scene.rs:152-244 in single precision, statistical parity with the f64 reference only
+// (DESIGN.md §10). Same RNG streams and draw order as the f64 kernels (one xoroshiro128++ stream per
+// camera sample, Philox-seeded; a draw is the top 24 bits of the same 64-bit output), so an f32
+// frame tracks the f64 frame path for path until a rounding difference flips a branch.
+//
+// Differences from the f64 path (all inside the statistical tolerance, tests/test_gpu_parity.py):
+//   * every hit point is offset by off32 * n (2^-16 of the scene's largest coordinate; the
+//     reference offsets planes and triangles by 1e-5 * n and spheres not at all) — 1e-5 is about one
+//     f32 ulp at the scenes' coordinates (~100) and would self-intersect;
+//   * sphere roots by the cancellation-free form r^2 - |op - b d|^2 (geometry.rs:512-545 uses
+//     b^2 - op.op + r^2, which loses ~all bits in f32 for rays leaving a sphere);
+//   * diffuse and mirror throughput updates in closed form (kd / p, ks / p: the f cos / (pdf p) of
+//     scene.rs:176-184 / :232-240 with pdf and cos cancelled);
+//   * meshes are intersected with nearest-triangle semantics (geometry.rs:886-903, the
+//     RT_FLAG_MESH_NEAREST branch) through the BVH with f32 boxes rounded outward.
+// Supported: diffuse and mirror BRDFs, sphere lights, spheres / planes / meshes, MIS on or off —
+// every reference scene. Phong and mesh lights are rejected on the host (rt_api.cpp).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "../device/integrator_f64.h"  // Rng, subpixel_of (integer work shared with the f64 path)
+#include "kernels.h"
+
+namespace rt {
+namespace f32 {
+
+#define RT_DEV32 __device__ __forceinline__
+
+struct F3 {
+    float x, y, z;
+};
+RT_DEV32 F3 f3(float x, float y, float z) { return F3{x, y, z}; }
+RT_DEV32 F3 ld3f(const float* p) { return F3{p[0], p[1], p[2]}; }
+RT_DEV32 F3 operator+(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+RT_DEV32 F3 operator-(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+RT_DEV32 F3 operator-(F3 a) { return f3(-a.x, -a.y, -a.z); }
+RT_DEV32 F3 operator*(F3 a, float s) { return f3(a.x * s, a.y * s, a.z * s); }
+RT_DEV32 F3 operator*(float s, F3 a) { return f3(a.x * s, a.y * s, a.z * s); }
+RT_DEV32 F3 mult(F3 a, F3 b) { return f3(a.x * b.x, a.y * b.y, a.z * b.z); }
+RT_DEV32 float dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+RT_DEV32 F3 cross(F3 a, F3 b) { return f3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+RT_DEV32 float rcp(float x) { return __builtin_amdgcn_rcpf(x); }  // 1 ulp
+RT_DEV32 F3 normalize(F3 a) { return a * __builtin_amdgcn_rsqf(dot(a, a)); }
+RT_DEV32 bool is_zero(F3 a) { return a.x == 0.f && a.y == 0.f && a.z == 0.f; }
+
+constexpr float INV_PI = 0.318309886183790671538f;
+constexpr float EPS_T = 1e-4f;  // sphere / triangle t threshold (geometry.rs:518, :667)
+
+RT_DEV32 float uni(f64::Rng& r) { return (float)(uint32_t)(r.next() >> 40) * 0x1p-24f; }
+
+struct Hit {
+    float t;
+    int obj, prim;  // prim: index into btris32 (mesh hits)
+};
+
+// Sphere::intersect (geometry.rs:512-545), cancellation-free discriminant.
+RT_DEV32 bool sphere_t(const Obj32& o, F3 ro, F3 rd, float* t) {
+    const F3 op = ld3f(o.pos) - ro;
+    const float b = dot(op, rd);
+    const F3 v = op - b * rd;
+    const float det = o.r2 - dot(v, v);
+    if (det < 0.f) return false;
+    const float s = __builtin_sqrtf(det);
+    float tt = b - s;
+    if (tt > EPS_T) { *t = tt; return true; }
+    tt = b + s;
+    if (tt > EPS_T) { *t = tt; return true; }
+    return false;
+}
+// Plane::intersect (geometry.rs:547-571).
+RT_DEV32 bool plane_t(const Obj32& o, F3 ro, F3 rd, float* t) {
+    const F3 n = ld3f(o.n);
+    const float dn = dot(rd, n);
+    if (__builtin_fabsf(dn) < 1e-4f) return false;
+    const float tt = dot(ld3f(o.pos) - ro, n) * rcp(dn);
+    if (tt >= 0.f) { *t = tt; return true; }
+    return false;
+}
+// Triangle::intersect (geometry.rs:637-670): Cramer's rule on (-d, ab, ac) as in the reference.
+RT_DEV32 bool tri_t(const Tri32& tr, F3 ro, F3 rd, float* t) {
+    const F3 n = ld3f(tr.n);
+    if (__builtin_fabsf(dot(n, rd)) < 1e-4f) return false;
+    const F3 ab = ld3f(tr.ab), ac = ld3f(tr.ac);
+    const F3 b = ro - ld3f(tr.a);
+    const F3 nd = -rd;
+    const F3 abac = cross(ab, ac);
+    const float det = dot(nd, abac);
+    const float y = rcp(det);
+    const float u = dot(nd, cross(b, ac)) * y;
+    const float v = dot(nd, cross(ab, b)) * y;
+    if (u < 0.f || u > 1.f || v < 0.f || u + v > 1.f) return false;
+    const float tt = dot(b, abac) * y;
+    if (tt > EPS_T) { *t = tt; return true; }
+    return false;
+}
+
+struct RayF {
+    F3 o, d, inv;
+};
+RT_DEV32 float safe_inv(float d) { return rcp(__builtin_fabsf(d) < 1e-30f ? __builtin_copysignf(1e-30f, d) : d); }
+RT_DEV32 RayF make_ray(F3 o, F3 d) { return RayF{o, d, f3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z))}; }
+
+RT_DEV32 bool box_hit(const Bvh32& nd, const RayF& r, float tmax) {
+    const float x0 = (nd.bmin[0] - r.o.x) * r.inv.x, x1 = (nd.bmax[0] - r.o.x) * r.inv.x;
+    const float y0 = (nd.bmin[1] - r.o.y) * r.inv.y, y1 = (nd.bmax[1] - r.o.y) * r.inv.y;
+    const float z0 = (nd.bmin[2] - r.o.z) * r.inv.z, z1 = (nd.bmax[2] - r.o.z) * r.inv.z;
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.f));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmax));
+    return tn <= tf;
+}
+
+// Per-lane BVH stack in LDS, one column per thread (blocks of 256).
+__shared__ int32_t s_stack32[kBvhMaxDepth * 256];
+
+// Nearest triangle of mesh m closer than *t (the Mesh::intersect `octree: None` loop,
+// geometry.rs:886-903, accelerated). any_hit: stop at the first triangle closer than *t.
+template <bool any_hit>
+RT_DEV32 bool mesh_t(const DevScene& sc, const DevMesh& m, const RayF& r, float* t, int* prim) {
+    if (m.bvh_n <= 0) return false;
+    __attribute__((address_space(3))) int32_t* stk = (__attribute__((address_space(3))) int32_t*)s_stack32 + threadIdx.x;
+    int cur = m.bvh_base, sp = 0;
+    bool found = false;
+    float best = *t;
+    while (true) {
+        const Bvh32 nd = sc.bvh32[cur];
+        if (box_hit(nd, r, best)) {
+            const int cnt = nd.cnt_axis >> 2;
+            if (cnt == 0) {
+                const int axis = nd.cnt_axis & 3;
+                const float dk = axis == 0 ? r.d.x : axis == 1 ? r.d.y : r.d.z;
+                const int l = cur + 1, rr = nd.a;
+                stk[sp * 256] = dk < 0.f ? l : rr;  // far child
+                ++sp;
+                cur = dk < 0.f ? rr : l;
+                continue;
+            }
+            for (int k = 0; k < cnt; ++k) {
+                float tt;
+                if (tri_t(sc.btris32[nd.a + k], r.o, r.d, &tt) && tt < best) {
+                    best = tt;
+                    *prim = nd.a + k;
+                    found = true;
+                }
+            }
+            if (any_hit && found) break;
+        }
+        if (sp == 0) break;
+        --sp;
+        cur = stk[sp * 256];
+    }
+    if (found) *t = best;
+    return found;
+}
+
+// Scene::trace_ray (scene.rs:272-289): nearest over all objects in index order, strict <.
+template <bool MESH>
+RT_DEV32 Hit trace_closest(const DevScene& sc, const RayF& r) {
+    Hit h{3.0e38f, -1, -1};
+    for (int i = 0; i < sc.n_objects; ++i) {
+        const Obj32& o = sc.obj32[i];
+        float t;
+        if (o.geom == GEOM_SPHERE) {
+            if (sphere_t(o, r.o, r.d, &t) && t < h.t) { h.t = t; h.obj = i; }
+        } else if (o.geom == GEOM_PLANE) {
+            if (plane_t(o, r.o, r.d, &t) && t < h.t) { h.t = t; h.obj = i; }
+        } else if constexpr (MESH) {
+            t = h.t;
+            int prim = -1;
+            if (mesh_t<false>(sc, sc.meshes[o.mesh], r, &t, &prim) && t < h.t) { h.t = t; h.obj = i; h.prim = prim; }
+        }
+    }
+    return h;
+}
+
+// Scene::mutually_visible (scene.rs:250-270) as an any-hit query: blocked iff some object's hit
+// satisfies t + 0.001 < |y - x|.
+template <bool MESH>
+RT_DEV32 bool visible(const DevScene& sc, const RayF& r, float dist) {
+    const float lim = dist - 0.001f;
+    for (int i = 0; i < sc.n_objects; ++i) {
+        const Obj32& o = sc.obj32[i];
+        float t;
+        if (o.geom == GEOM_SPHERE) {
+            if (sphere_t(o, r.o, r.d, &t) && t < lim) return false;
+        } else if (o.geom == GEOM_PLANE) {
+            if (plane_t(o, r.o, r.d, &t) && t < lim) return false;
+        } else if constexpr (MESH) {
+            t = lim;
+            int prim;
+            if (lim > 0.f && mesh_t<true>(sc, sc.meshes[o.mesh], r, &t, &prim)) return false;
+        }
+    }
+    return true;
+}
+
+enum : int { K_CAMERA = 0, K_SPEC = 1, K_DIFF = 2 };
+
+struct Path {
+    F3 ro, rd, beta, L, bemit, o;
+    float pdf_prev;
+    uint64_t r0, r1;
+    uint32_t depth;
+    int kind;
+};
+
+struct Cam {
+    F3 pos, dir, cx, cy;
+    float w, h;
+};
+
+// sample_pixel's camera ray (server.rs:338-357) for sample `smp` of tile subpixel `id`.
+RT_DEV32 void begin_sample(const Cam& cam, const RenderArgs& a, long id, int smp, Path& ps) {
+    const f64::SubPixel sp = f64::subpixel_of(a, id);
+    f64::Rng rng(a.seed, sp.pid, (uint32_t)smp, (uint32_t)sp.sub);
+    const float u1 = uni(rng), u2 = uni(rng);
+    const float r1 = 2.f * u1, r2 = 2.f * u2;
+    const float dx = r1 < 1.f ? __builtin_sqrtf(r1) - 1.f : 1.f - __builtin_sqrtf(2.f - r1);
+    const float dy = r2 < 1.f ? __builtin_sqrtf(r2) - 1.f : 1.f - __builtin_sqrtf(2.f - r2);
+    const F3 d = cam.cx * ((((float)sp.sx + 0.5f + dx) * 0.5f + (float)sp.col) / cam.w - 0.5f) +
+                 cam.cy * ((((float)sp.sy + 0.5f + dy) * 0.5f + (float)sp.yref) / cam.h - 0.5f) + cam.dir;
+    ps.ro = cam.pos;
+    ps.rd = normalize(d);
+    ps.r0 = rng.s0;
+    ps.r1 = rng.s1;
+    ps.beta = f3(1.f, 1.f, 1.f);
+    ps.L = f3(0.f, 0.f, 0.f);
+    ps.bemit = f3(0.f, 0.f, 0.f);
+    ps.o = f3(0.f, 0.f, 0.f);
+    ps.pdf_prev = 0.f;
+    ps.depth = 0;
+    ps.kind = K_CAMERA;
+}
+
+// One path vertex (integrator_f64.h: shade_vertex, same walk and draw order). Returns true when the
+// path continues with ps.ro / ps.rd.
+template <bool MESH, bool MIS>
+RT_DEV32 bool shade(const DevScene& sc, Path& ps, const Hit& h, float light_pdf) {
+    if (h.obj < 0) return false;
+    const Obj32& obj = sc.obj32[h.obj];
+    F3 x = ps.ro + h.t * ps.rd, n;
+    if (obj.geom == GEOM_SPHERE) n = normalize(x - ld3f(obj.pos));
+    else if (obj.geom == GEOM_PLANE) n = ld3f(obj.n);
+    else n = ld3f(sc.btris32[h.prim].n);
+    if (dot(n, ps.rd) > 0.f) n = -n;  // normal toward the incoming side (geometry.rs:535, :566, :669)
+    x = x + n * sc.off32;
+    const F3 Le = ld3f(obj.emitted);
+    if (ps.kind == K_CAMERA) {
+        ps.L = Le;
+    } else if (ps.kind == K_SPEC) {
+        ps.L = ps.L + mult(ps.bemit, Le);
+    } else if (MIS && h.obj == sc.light && ps.pdf_prev > 0.f) {
+        const float cosl = -dot(n, ps.rd);
+        const float pdf_l = light_pdf * (h.t * h.t) / cosl;
+        ps.L = ps.L + mult(ps.beta, Le * (ps.pdf_prev / (ps.pdf_prev + pdf_l)));
+    }
+    if (ps.kind != K_SPEC) ps.o = -ps.rd;
+    ps.depth += 1;
+    const float p = ps.depth <= (uint32_t)f64::MAX_BOUNCES ? 1.f : (float)f64::SURVIVAL_PROBABILITY;
+    f64::Rng rng(ps.r0, ps.r1);
+    const bool spec = obj.brdf == BRDF_SPECULAR;
+    const F3 k = ld3f(obj.k);
+    if (!spec) {
+        // next-event estimation to the sphere light (scene.rs:217-229, geometry.rs:573-585)
+        const Obj32& Lo = sc.obj32[sc.light];
+        const float xi1 = uni(rng), xi2 = uni(rng);
+        const float z = 2.f * xi1 - 1.f;
+        float sphi, cphi;
+        __sincosf(6.283185307179586f * xi2, &sphi, &cphi);
+        const float sz = __builtin_sqrtf(fmaxf(0.f, 1.f - z * z));
+        const F3 ny = f3(sz * cphi, sz * sphi, z);
+        const F3 y = ld3f(Lo.pos) + ny * Lo.r;
+        const F3 diff = y - x;
+        const float r_sqr = dot(diff, diff);
+        const float dist = __builtin_sqrtf(r_sqr);
+        const F3 i = diff * rcp(dist);
+        const F3 lef = mult(ld3f(Lo.emitted), k) * INV_PI;
+        if (!is_zero(lef)) {
+            const bool vis = visible<MESH>(sc, make_ray(x, i), dist);
+            const float cosx = dot(n, i), cosl = -dot(ny, i);
+            F3 c = f3(0.f, 0.f, 0.f);
+            if (!MIS) {
+                if (vis) c = lef * (cosx * cosl / (r_sqr * light_pdf));
+            } else {
+                const float pdf_l = light_pdf * r_sqr / cosl;
+                const float pdf_b = cosx * INV_PI;
+                if (vis && cosl > 0.f && pdf_b > 0.f) c = lef * (cosx / (pdf_l + pdf_b));
+            }
+            ps.L = ps.L + mult(ps.beta, c);
+        }
+    }
+    // Russian roulette + BSDF continuation (scene.rs:173-184 / :231-242)
+    if (!(uni(rng) < p)) return false;
+    F3 wi;
+    float pdf = 0.f;
+    if (!spec) {
+        const float z = __builtin_sqrtf(uni(rng));
+        const float rr = __builtin_sqrtf(fmaxf(0.f, 1.f - z * z));
+        float sphi, cphi;
+        __sincosf(6.283185307179586f * uni(rng), &sphi, &cphi);
+        // create_local_coord (scene.rs:112-123)
+        const F3 base = __builtin_fabsf(n.x) > 0.1f ? f3(0.f, 1.f, 0.f) : f3(1.f, 0.f, 0.f);
+        const F3 u = normalize(cross(base, n));
+        const F3 v = cross(n, u);
+        wi = normalize(u * (rr * cphi) + v * (rr * sphi) + n * z);
+        pdf = dot(n, wi) * INV_PI;
+    } else {
+        wi = (2.f * dot(ps.o, n)) * n - ps.o;  // o.flip_across(n) (scene.rs:50-54)
+        ps.bemit = ps.beta;
+    }
+    ps.r0 = rng.s0;
+    ps.r1 = rng.s1;
+    ps.beta = mult(ps.beta, k) * rcp(p);
+    ps.ro = x;
+    ps.rd = wi;
+    ps.kind = spec ? K_SPEC : K_DIFF;
+    ps.pdf_prev = MIS && !spec ? pdf : 0.f;
+    return spec || !is_zero(ps.beta);
+}
+
+RT_DEV32 long wave_ticket(uint32_t* counter, bool want) {
+    const unsigned long long m = __ballot(want);
+    if (m == 0ull) return -1;
+    const int lane = __lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+    return want ? (long)base + __popcll(below) : -1;
+}
+
+// Persistent path loop: a resident grid whose lanes take subpixels from a global counter and walk
+// their spp/4 samples vertex by vertex (a finished sample starts the next one in the next
+// iteration). The subpixel mean is written in f64 for k_finalize_f64 (clamp, gamma, `as u8`).
+template <bool MESH, bool MIS>
+__global__ __launch_bounds__(256) void k_megakernel_f32(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
+                                                       uint32_t* next_sub, long nsub) {
+    Cam cam;
+    cam.pos = f3((float)sc.cam_pos[0], (float)sc.cam_pos[1], (float)sc.cam_pos[2]);
+    cam.dir = f3((float)sc.cam_dir[0], (float)sc.cam_dir[1], (float)sc.cam_dir[2]);
+    cam.cx = f3((float)a.cx[0], (float)a.cx[1], (float)a.cx[2]);
+    cam.cy = f3((float)a.cy[0], (float)a.cy[1], (float)a.cy[2]);
+    cam.w = (float)a.width;
+    cam.h = (float)a.height;
+    const float light_pdf = (float)sc.light_pdf;
+    uint32_t nverts = 0;
+    long id = wave_ticket(next_sub, true);
+    bool active = id < nsub;
+    int smp = 0;
+    F3 acc = f3(0.f, 0.f, 0.f);
+    Path ps;
+    if (active) begin_sample(cam, a, id, 0, ps);
+    while (__any(active)) {
+        bool finished = false;
+        if (active) {
+            const Hit h = trace_closest<MESH>(sc, make_ray(ps.ro, ps.rd));
+            nverts += h.obj >= 0;
+            if (!shade<MESH, MIS>(sc, ps, h, light_pdf)) {
+                acc = acc + ps.L;
+                if (++smp < a.n_samples) {
+                    begin_sample(cam, a, id, smp, ps);
+                } else {
+                    double* o = sub_buf + (size_t)id * 3;
+                    o[0] = (double)acc.x * a.inv_n;
+                    o[1] = (double)acc.y * a.inv_n;
+                    o[2] = (double)acc.z * a.inv_n;
+                    finished = true;
+                }
+            }
+        }
+        const long t = wave_ticket(next_sub, finished && !(a.cancel && *(const volatile int32_t*)a.cancel));
+        if (finished) {
+            if (t >= 0 && t < nsub) {
+                id = t;
+                smp = 0;
+                acc = f3(0.f, 0.f, 0.f);
+                begin_sample(cam, a, id, 0, ps);
+            } else {
+                active = false;
+            }
+        }
+    }
+    if (a.counters) {
+        unsigned long long v = nverts;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (__lane_id() == 0 && v) atomicAdd(a.counters, v);
+    }
+}
+
+template <bool MESH, bool MIS>
+static hipError_t launch_k(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
+                           hipStream_t st) {
+    auto kern = k_megakernel_f32<MESH, MIS>;
+    int dev = 0, ncu = 256, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    const long blocks = std::max(1L, std::min((long)ncu * per_cu, (nsub + 255) / 256));
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub, nsub);
+    return hipGetLastError();
+}
+
+}  // namespace f32
+
+hipError_t launch_megakernel_f32(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
+                                 hipStream_t st) {
+    const long nsub = (long)a.tw * a.th * 4;
+    if (nsub <= 0 || a.n_samples <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(next_sub, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    const bool mesh = (a.features & 1) != 0, mis = a.mis != 0;
+    if (mesh) return mis ? f32::launch_k<true, true>(sc, a, sub_buf, next_sub, nsub, st)
+                         : f32::launch_k<true, false>(sc, a, sub_buf, next_sub, nsub, st);
+    return mis ? f32::launch_k<false, true>(sc, a, sub_buf, next_sub, nsub, st)
+               : f32::launch_k<false, false>(sc, a, sub_buf, next_sub, nsub, st);
+}
+
+}  // namespace rt

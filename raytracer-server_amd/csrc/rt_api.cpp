@@ -287,6 +287,69 @@ void fill_compact(const Packed& p, rt::CompactTab* ds, int32_t* compact) {
     ds->n_gen = ok ? ng : 0;
 }
 
+// f32 perf-mode tables (scene_layout.h: Obj32 / Bvh32 / Tri32). BVH boxes are rounded outward and
+// padded by a few f32 ulps of their largest coordinate, so the f32 slab test never culls a box the
+// f64 one would enter; off32 (the hit-point offset) is 2^-16 of the scene's largest coordinate.
+float f32_down(double x) {
+    float f = (float)x;
+    if ((double)f > x) f = std::nextafter(f, -INFINITY);
+    return f;
+}
+float f32_up(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = std::nextafter(f, INFINITY);
+    return f;
+}
+void pack_f32(const Packed& p, std::vector<rt::Obj32>* objs, std::vector<rt::Bvh32>* bvh,
+              std::vector<rt::Tri32>* tris, float* off32) {
+    double scale = 1.0;
+    auto grow = [&](double v) { scale = std::max(scale, std::fabs(v)); };
+    for (const auto& o : p.objects) {
+        rt::Obj32 q{};
+        q.geom = o.geom;
+        q.brdf = o.brdf;
+        q.mesh = o.mesh;
+        q.emissive = o.emissive;
+        for (int k = 0; k < 3; ++k) {
+            q.emitted[k] = (float)o.emitted[k];
+            q.k[k] = (float)o.k[k];
+            q.pos[k] = (float)o.pos[k];
+            q.n[k] = (float)o.n[k];
+            if (o.geom == rt::GEOM_SPHERE) grow(std::fabs(o.pos[k]) + o.r);
+            else if (o.geom == rt::GEOM_PLANE && o.n[k] != 0.0) grow(o.pos[k]);
+        }
+        q.r = (float)o.r;
+        q.r2 = (float)(o.r * o.r);
+        objs->push_back(q);
+    }
+    for (const auto& m : p.meshes)
+        for (int k = 0; k < 6; ++k) grow(m.root_box[k]);
+    for (const auto& n : p.bvh) {
+        rt::Bvh32 q{};
+        double pad = 0.0;
+        for (int k = 0; k < 3; ++k) pad = std::max({pad, std::fabs(n.bmin[k]), std::fabs(n.bmax[k])});
+        pad *= 0x1p-20;
+        for (int k = 0; k < 3; ++k) {
+            q.bmin[k] = f32_down(n.bmin[k] - pad);
+            q.bmax[k] = f32_up(n.bmax[k] + pad);
+        }
+        q.a = n.a;
+        q.cnt_axis = n.count * 4 + n.axis;
+        bvh->push_back(q);
+    }
+    for (const auto& t : p.btris) {
+        rt::Tri32 q{};
+        for (int k = 0; k < 3; ++k) {
+            q.a[k] = (float)t.a[k];
+            q.ab[k] = (float)t.ab[k];
+            q.ac[k] = (float)t.ac[k];
+            q.n[k] = (float)t.n[k];
+        }
+        tris->push_back(q);
+    }
+    *off32 = (float)std::max(1e-5, scale * 0x1p-16);
+}
+
 template <class T>
 void put(std::vector<char>& blob, size_t* off, const std::vector<T>& v) {
     *off = align_up(blob.size(), 256);
@@ -302,6 +365,12 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         const Packed& p = s->packed;
         std::vector<char> blob;
         size_t o_obj, o_mesh, o_kids, o_up, o_leaf, o_ltri, o_lid, o_tris, o_cum, o_tab, o_bvh, o_btri, o_bid;
+        size_t o_obj32, o_bvh32, o_tri32;
+        std::vector<rt::Obj32> obj32;
+        std::vector<rt::Bvh32> bvh32;
+        std::vector<rt::Tri32> tri32;
+        float off32 = 0.f;
+        pack_f32(p, &obj32, &bvh32, &tri32, &off32);
         std::vector<rt::CompactTab> tab(1);
         std::memset(tab.data(), 0, sizeof(rt::CompactTab));
         int32_t compact = 0;
@@ -319,6 +388,9 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         put(blob, &o_bvh, p.bvh);
         put(blob, &o_btri, p.btris);
         put(blob, &o_bid, p.btri_id);
+        put(blob, &o_obj32, obj32);
+        put(blob, &o_bvh32, bvh32);
+        put(blob, &o_tri32, tri32);
         void* d = nullptr;
         HIP_TRY(hipMalloc(&d, blob.size()));
         hipError_t e = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice);
@@ -342,6 +414,10 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.bvh = (const rt::DevBvhNode*)(b + o_bvh);
         ds.btris = (const rt::DevTri*)(b + o_btri);
         ds.btri_id = (const int32_t*)(b + o_bid);
+        ds.obj32 = (const rt::Obj32*)(b + o_obj32);
+        ds.bvh32 = (const rt::Bvh32*)(b + o_bvh32);
+        ds.btris32 = (const rt::Tri32*)(b + o_tri32);
+        ds.off32 = off32;
         ds.compact = compact;
         ds.light = s->host.light;
         ds.light_pdf = 0.0;
@@ -423,8 +499,16 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
     a.inv_n = a.n_samples > 0 ? 1. / (double)a.n_samples : 0.0;
     a.sub_out = d_sub;
     a.rgb_out = d_rgb;
-    if (p->flags & RT_FLAG_FP32) return fail(RT_E_INVAL, "RT_FLAG_FP32 is not available in this build");
-    if ((p->flags & RT_FLAG_MESH_NEAREST) && !(p->flags & RT_FLAG_MEGAKERNEL))
+    const bool fp32 = (p->flags & RT_FLAG_FP32) != 0;
+    if (fp32) {
+        // the f32 kernel covers diffuse / mirror BRDFs and sphere lights (every reference scene)
+        for (const auto& o : s->host.objects)
+            if (o.brdf == RT_BRDF_PHONG) return fail(RT_E_INVAL, "RT_FLAG_FP32: Phong BRDFs need the f64 path");
+        const auto& L = s->packed.objects;
+        if (ds.light >= 0 && ds.light < (int32_t)L.size() && L[ds.light].geom != rt::GEOM_SPHERE)
+            return fail(RT_E_INVAL, "RT_FLAG_FP32: only sphere lights (mesh lights need the f64 path)");
+    }
+    if (!fp32 && (p->flags & RT_FLAG_MESH_NEAREST) && !(p->flags & RT_FLAG_MEGAKERNEL))
         return fail(RT_E_INVAL, "RT_FLAG_MESH_NEAREST needs RT_FLAG_MEGAKERNEL");
     std::unique_ptr<rt::Workspace> ws = take_workspace(s, p->device);
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -436,7 +520,7 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
     }
     int out = RT_OK;
     std::string err;
-    if (p->flags & RT_FLAG_MEGAKERNEL) {
+    if (fp32 || (p->flags & RT_FLAG_MEGAKERNEL)) {
         const size_t npix = (size_t)p->tile_w * p->tile_h;
         // device view of the caller's cancel flag: the megakernel polls it between subpixels
         void* dcancel = nullptr;
@@ -463,10 +547,14 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
             // split-tail scratch: up to one subpixel per resident lane, at most 1.5 GB
             const size_t per_sub = (size_t)std::max(0, a.n_samples) * 3 * sizeof(double);
             const size_t want = std::min<size_t>((size_t)3 << 29, per_sub * std::min<size_t>(npix * 4 / 2, (size_t)1 << 19));
-            if (per_sub > 0 && want >= per_sub) {
+            if (!fp32 && per_sub > 0 && want >= per_sub) {
                 if (ws->ensure_tail(want) != hipSuccess) (void)hipGetLastError();  // no tail split then
             }
-            e = rt::launch_megakernel_f64(ds, a, sub, (uint32_t*)(ws->counters + 4), ws->tail_buf, ws->tail_cap, st);
+            if (fp32) {
+                e = rt::launch_megakernel_f32(ds, a, sub, (uint32_t*)(ws->counters + 4), st);
+            } else {
+                e = rt::launch_megakernel_f64(ds, a, sub, (uint32_t*)(ws->counters + 4), ws->tail_buf, ws->tail_cap, st);
+            }
         }
         if (e == hipSuccess) e = rt::launch_finalize_f64(a, sub, st);
         if (e != hipSuccess) { out = RT_E_HIP; err = std::string("megakernel: ") + hipGetErrorString(e); }
@@ -485,7 +573,7 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
         if (e == hipSuccess) e = hipEventSynchronize(e1);
         float ms = 0.f;
         if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
-        if (e == hipSuccess && (p->flags & RT_FLAG_MEGAKERNEL)) {
+        if (e == hipSuccess && (fp32 || (p->flags & RT_FLAG_MEGAKERNEL))) {
             unsigned long long cnt[1] = {0};
             e = hipMemcpy(cnt, ws->counters, sizeof cnt, hipMemcpyDeviceToHost);
             stats->vertices = (int64_t)cnt[0];

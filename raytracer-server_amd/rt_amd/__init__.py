@@ -245,10 +245,12 @@ def make_params(width, height, spp, seed=0x5EED, tile=None, flags=0, device=0, r
 
 
 def render(scene, width, height, spp, seed=0x5EED, tile=None, mis=False, megakernel=False, device=0,
-           want_sub=False, cancel=None, row_step=1, mesh_nearest=False):
+           want_sub=False, cancel=None, row_step=1, mesh_nearest=False, fp32=False):
     """Renders a tile to host memory. Returns (rgb[th, tw, 3] u8, sub[th, tw, 4, 3] f64 or None, stats).
-    mesh_nearest: Mesh::intersect's `octree: None` semantics (RT_FLAG_MESH_NEAREST, megakernel only)."""
+    mesh_nearest: Mesh::intersect's `octree: None` semantics (RT_FLAG_MESH_NEAREST, megakernel only).
+    fp32: the f32 perf mode (RT_FLAG_FP32: statistical parity only; meshes with nearest-triangle semantics)."""
     flags = (FLAG_MIS if mis else 0) | (FLAG_MEGAKERNEL if megakernel else 0) | (FLAG_MESH_NEAREST if mesh_nearest else 0)
+    flags |= FLAG_FP32 if fp32 else 0
     p = make_params(width, height, spp, seed, tile, flags, device, row_step)
     rgb = np.zeros((p.tile_h, p.tile_w, 3), dtype=np.uint8)
     sub = np.zeros((p.tile_h, p.tile_w, 4, 3), dtype=np.float64) if want_sub else None

@@ -234,3 +234,70 @@ def test_cancel(rt, gpu_scenes, megakernel):
     dt = time.time() - t0
     timer.cancel()
     assert st["cancelled"] and dt < 4.0, (st["cancelled"], dt)
+
+
+# ---------------------------------------------------------------- f32 perf mode (RT_FLAG_FP32)
+# Statistical parity only. The f32 kernel draws the same RNG streams in the same
+# order (a draw is the top 24 bits of the f64 draw's 64-bit word), so its frame tracks the f64 frame
+# path for path and the comparison is paired, pixel by pixel. Bounds (measured margins in DESIGN.md §10,
+# profiles/r01h_fp32.log):
+#   * per-channel image mean of the pixel values: |rel| <= 0.5%;
+#   * 16x16-block means: |diff| <= 4 paired standard errors, or <= 1% of the block mean;
+#   * RGB8 within 1 on >= 93% of pixels, mean |dRGB8| <= 0.3.
+def _assert_fp32_stats(sub_f, sub_r, rgb_f, rgb_r, what):
+    cf = np.clip(sub_f, 0, 1).mean(axis=2)  # pixel values before gamma (server.rs:358-360)
+    cr = np.clip(sub_r, 0, 1).mean(axis=2)
+    m_f, m_r = cf.mean(axis=(0, 1)), cr.mean(axis=(0, 1))
+    assert np.all(np.abs(m_f - m_r) <= 0.005 * m_r), f"{what}: image means {m_f} vs {m_r}"
+    h, w = cf.shape[:2]
+    B = 16
+    hb, wb = h // B, w // B
+    d = (cf - cr)[:hb * B, :wb * B].reshape(hb, B, wb, B, 3)
+    bm = np.abs(d.mean(axis=(1, 3)))
+    se = d.std(axis=(1, 3)) / B
+    ref = cr[:hb * B, :wb * B].reshape(hb, B, wb, B, 3).mean(axis=(1, 3))
+    bad = (bm > 4 * se) & (bm > 0.01 * np.maximum(ref, 1e-3))
+    assert bad.mean() <= 0.01, f"{what}: {np.count_nonzero(bad)} of {bad.size} block means off"
+    diff = np.abs(rgb_f.astype(int) - rgb_r.astype(int))
+    assert np.all(diff <= 1, axis=-1).mean() >= 0.93, f"{what}: RGB8 within 1 on too few pixels"
+    assert diff.mean() <= 0.3, f"{what}: mean |dRGB8| {diff.mean():.3f}"
+
+
+@pytest.mark.parametrize("name,mis", [("cornell_box", False), ("cornell_box", True), ("cubes", False),
+                                      ("cubes", True)])
+def test_fp32_statistical_parity(name, mis, rt, gpu_scenes, oracle_scenes, oracle_nearest):
+    w, h, spp = 96, 80, 64
+    rgb_f, sub_f, st = rt.render(gpu_scenes[name], w, h, spp, SEED, mis=mis, want_sub=True, fp32=True)
+    assert st["samples"] == w * h * spp
+    # cubes: the convex cubes give the same hits under both mesh semantics (test_trace_mesh_nearest_bit_exact)
+    ref = oracle_scenes[name]
+    rgb_o, sub_o, st_o = ref.render(w, h, spp, SEED, mis=mis)
+    # the GPU ends zero-throughput paths early (the oracle keeps walking them, at zero radiance)
+    assert 0.9 * st_o["vertices"] <= st["vertices"] <= 1.01 * st_o["vertices"]
+    _assert_fp32_stats(sub_f, sub_o, rgb_f, rgb_o, f"{name}/f32{'/mis' if mis else ''}")
+
+
+def test_fp32_statistical_parity_mesh(rt, gpu_scenes, oracle_nearest):
+    """The unicorn in f32 (nearest-triangle meshes) against the f64 nearest-triangle path, which is
+    bit-exact against the oracle's brute-force loop (test_render_parity_mesh_nearest), at a size the
+    brute-force oracle cannot reach; plus a direct oracle check on a small tile."""
+    sc = gpu_scenes["flying_unicorn"]
+    w, h, spp = 192, 144, 64
+    rgb_f, sub_f, st = rt.render(sc, w, h, spp, SEED, want_sub=True, fp32=True)
+    rgb_d, sub_d, st_d = rt.render(sc, w, h, spp, SEED, want_sub=True, megakernel=True, mesh_nearest=True)
+    assert abs(st["vertices"] / st_d["vertices"] - 1) < 0.01
+    _assert_fp32_stats(sub_f, sub_d, rgb_f, rgb_d, "flying_unicorn/f32")
+    rgb_f, sub_f, _ = rt.render(sc, 24, 18, 4, SEED, want_sub=True, fp32=True)
+    rgb_o, sub_o, _ = oracle_nearest["flying_unicorn"].render(24, 18, 4, SEED)
+    assert np.all(np.abs(rgb_f.astype(int) - rgb_o.astype(int)) <= 1, axis=-1).mean() >= 0.8
+
+
+def test_fp32_rejects_unsupported(rt, gpu_scenes):
+    """Phong BRDFs and mesh lights stay on the f64 path: RT_FLAG_FP32 returns RT_E_INVAL for them."""
+    phong = rt.Scene.from_desc([50, 52, 295.6], [0, -0.042612, -1], [
+        dict(geom_kind=1, pos=[0, 0, 0], n=[0, 1, 0], brdf_kind=2, phong_kd=0.5, phong_ks=0.3, phong_power=8,
+             color_d=[0.7, 0.7, 0.7], color_s=[1, 1, 1]),
+        dict(geom_kind=0, pos=[50, 70, 100], r=4, brdf_kind=0, k=[0, 0, 0], emitted=[50, 50, 50])])
+    with pytest.raises(rt.RtError):
+        rt.render(phong, 8, 8, 4, SEED, fp32=True)
+    rt.render(phong, 8, 8, 4, SEED)  # the f64 path renders it
