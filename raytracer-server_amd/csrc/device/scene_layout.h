@@ -96,7 +96,8 @@ struct alignas(16) Obj32 {
     int32_t geom, brdf, mesh, emissive;
     float emitted[3], r;
     float k[3], r2;       // kd / ks; sphere radius squared
-    float pos[3], pad0;
+    float pos[3];
+    int32_t axis;         // plane with n = +-e_axis (0, 1, 2), else -1
     float n[3], pad1;
 };
 struct alignas(16) Bvh32 {
@@ -107,6 +108,16 @@ struct alignas(16) Bvh32 {
 };
 struct Tri32 {
     float a[3], ab[3], ac[3], n[3];
+};
+
+// CompactTab in f32 (built from it): the trace loops' operands in one scalar-loadable block.
+struct Compact32 {
+    int32_t n_ax[3], n_sph, n_gen, ok;
+    int32_t ax_idx[3][kMaxAxisPlanes];
+    float ax_pos[3][kMaxAxisPlanes];
+    int32_t sph_idx[kMaxSpheres];
+    float sph[kMaxSpheres][4];  // centre xyz, r*r
+    int32_t gen_idx[kMaxGeneric];
 };
 
 struct DevScene {
@@ -127,6 +138,7 @@ struct DevScene {
     const Obj32* obj32;         // f32 perf mode tables (Obj32 / Bvh32 / Tri32 above)
     const Bvh32* bvh32;
     const Tri32* btris32;
+    const Compact32* ctab32;    // f32 compact tables (ok == 0: the generic object loop)
     float off32;                // f32 mode: hit points are offset by off32 * n (scene-scaled epsilon)
     int32_t n_objects, light, n_meshes, compact;
     double cam_pos[3], cam_dir[3];

@@ -19,9 +19,17 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "../device/integrator_f64.h"  // Rng, subpixel_of (integer work shared with the f64 path)
 #include "kernels.h"
+
+#ifndef RT_F32_W
+#define RT_F32_W 4       // waves/SIMD, analytic scenes
+#endif
+#ifndef RT_F32_W_MESH
+#define RT_F32_W_MESH 8  // waves/SIMD, scenes with deep meshes
+#endif
 
 namespace rt {
 namespace f32 {
@@ -42,11 +50,20 @@ RT_DEV32 F3 mult(F3 a, F3 b) { return f3(a.x * b.x, a.y * b.y, a.z * b.z); }
 RT_DEV32 float dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 RT_DEV32 F3 cross(F3 a, F3 b) { return f3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
 RT_DEV32 float rcp(float x) { return __builtin_amdgcn_rcpf(x); }  // 1 ulp
+RT_DEV32 float sqrt_a(float x) { return __builtin_amdgcn_sqrtf(x); }  // v_sqrt_f32, 1 ulp (no denormal scaling)
 RT_DEV32 F3 normalize(F3 a) { return a * __builtin_amdgcn_rsqf(dot(a, a)); }
 RT_DEV32 bool is_zero(F3 a) { return a.x == 0.f && a.y == 0.f && a.z == 0.f; }
 
 constexpr float INV_PI = 0.318309886183790671538f;
 constexpr float EPS_T = 1e-4f;  // sphere / triangle t threshold (geometry.rs:518, :667)
+
+// The object table through the constant address space: with a wave-uniform index (readfirstlane)
+// the object loops read it with scalar loads instead of one vector load chain per object.
+typedef const __attribute__((address_space(4))) Obj32 CObj;
+RT_DEV32 CObj& obj_u(const DevScene& sc, int i) {
+    return ((CObj*)sc.obj32)[__builtin_amdgcn_readfirstlane(i)];
+}
+RT_DEV32 F3 ld3c(const __attribute__((address_space(4))) float* p) { return F3{p[0], p[1], p[2]}; }
 
 RT_DEV32 float uni(f64::Rng& r) { return (float)(uint32_t)(r.next() >> 40) * 0x1p-24f; }
 
@@ -56,13 +73,26 @@ struct Hit {
 };
 
 // Sphere::intersect (geometry.rs:512-545), cancellation-free discriminant.
-RT_DEV32 bool sphere_t(const Obj32& o, F3 ro, F3 rd, float* t) {
-    const F3 op = ld3f(o.pos) - ro;
+RT_DEV32 bool sphere_t(CObj& o, F3 ro, F3 rd, float* t) {
+    const F3 op = ld3c(o.pos) - ro;
     const float b = dot(op, rd);
     const F3 v = op - b * rd;
     const float det = o.r2 - dot(v, v);
     if (det < 0.f) return false;
-    const float s = __builtin_sqrtf(det);
+    const float s = sqrt_a(det);
+    float tt = b - s;
+    if (tt > EPS_T) { *t = tt; return true; }
+    tt = b + s;
+    if (tt > EPS_T) { *t = tt; return true; }
+    return false;
+}
+RT_DEV32 bool sphere_c(float cx, float cy, float cz, float r2, F3 ro, F3 rd, float* t) {
+    const F3 op = f3(cx, cy, cz) - ro;
+    const float b = dot(op, rd);
+    const F3 v = op - b * rd;
+    const float det = r2 - dot(v, v);
+    if (det < 0.f) return false;
+    const float s = sqrt_a(det);
     float tt = b - s;
     if (tt > EPS_T) { *t = tt; return true; }
     tt = b + s;
@@ -70,13 +100,33 @@ RT_DEV32 bool sphere_t(const Obj32& o, F3 ro, F3 rd, float* t) {
     return false;
 }
 // Plane::intersect (geometry.rs:547-571).
-RT_DEV32 bool plane_t(const Obj32& o, F3 ro, F3 rd, float* t) {
-    const F3 n = ld3f(o.n);
+RT_DEV32 bool plane_t(CObj& o, F3 ro, F3 rd, float* t) {
+    const F3 n = ld3c(o.n);
     const float dn = dot(rd, n);
     if (__builtin_fabsf(dn) < 1e-4f) return false;
-    const float tt = dot(ld3f(o.pos) - ro, n) * rcp(dn);
+    const float tt = dot(ld3c(o.pos) - ro, n) * rcp(dn);
     if (tt >= 0.f) { *t = tt; return true; }
     return false;
+}
+// Axis plane (n = +-e_K): dot(pos - o, n) / dot(d, n) = (pos_K - o_K) / d_K with the ray's reciprocal.
+template <int K>
+RT_DEV32 float comp(F3 v) { return K == 0 ? v.x : K == 1 ? v.y : v.z; }
+template <int K>
+RT_DEV32 bool axis_t(CObj& o, F3 ro, F3 rd, F3 inv, float* t) {
+    if (__builtin_fabsf(comp<K>(rd)) < 1e-4f) return false;
+    const float tt = (o.pos[K] - comp<K>(ro)) * comp<K>(inv);
+    if (tt >= 0.f) { *t = tt; return true; }
+    return false;
+}
+// Shadow segment x -> y against an axis plane: only a plane with x and y not strictly on one side
+// can block (behind x its t < 0, beyond y its t > |y - x|).
+template <int K>
+RT_DEV32 bool axis_blocks(CObj& o, F3 x, F3 y, F3 rd, F3 inv, float lim) {
+    const float sx = comp<K>(x) - o.pos[K], sy = comp<K>(y) - o.pos[K];
+    if ((sx > 0.f && sy > 0.f) || (sx < 0.f && sy < 0.f)) return false;
+    if (__builtin_fabsf(comp<K>(rd)) < 1e-4f) return false;
+    const float tt = -sx * comp<K>(inv);
+    return tt >= 0.f && tt < lim;
 }
 // Triangle::intersect (geometry.rs:637-670): Cramer's rule on (-d, ab, ac) as in the reference.
 RT_DEV32 bool tri_t(const Tri32& tr, F3 ro, F3 rd, float* t) {
@@ -117,7 +167,9 @@ __shared__ int32_t s_stack32[kBvhMaxDepth * 256];
 // Nearest triangle of mesh m closer than *t (the Mesh::intersect `octree: None` loop,
 // geometry.rs:886-903, accelerated). any_hit: stop at the first triangle closer than *t.
 template <bool any_hit>
-RT_DEV32 bool mesh_t(const DevScene& sc, const DevMesh& m, const RayF& r, float* t, int* prim) {
+RT_DEV32 bool mesh_t(const DevScene& sc, int mesh, const RayF& r, float* t, int* prim) {
+    typedef const __attribute__((address_space(4))) DevMesh CMesh;
+    CMesh& m = ((CMesh*)sc.meshes)[__builtin_amdgcn_readfirstlane(mesh)];
     if (m.bvh_n <= 0) return false;
     __attribute__((address_space(3))) int32_t* stk = (__attribute__((address_space(3))) int32_t*)s_stack32 + threadIdx.x;
     int cur = m.bvh_base, sp = 0;
@@ -154,21 +206,88 @@ RT_DEV32 bool mesh_t(const DevScene& sc, const DevMesh& m, const RayF& r, float*
     return found;
 }
 
-// Scene::trace_ray (scene.rs:272-289): nearest over all objects in index order, strict <.
+typedef const __attribute__((address_space(4))) Compact32 CTab32;
+// Per-call view of the compact tables: the empty asm makes the pointer opaque, so their scalar
+// loads are issued inside each trace call, not hoisted out of the path loop into ~60 live SGPRs.
+RT_DEV32 CTab32& tables32(const DevScene& sc) {
+    uint64_t p = (uint64_t)(uintptr_t)sc.ctab32;
+    asm volatile("" : "+s"(p));
+    return *(CTab32*)p;
+}
+
+// Nearest-hit update with the reference's tie rule (scene.rs:278: strict <, so ties go to the lower
+// index) — needed because the compact tables visit objects grouped by type.
+RT_DEV32 void consider(Hit& h, float t, int idx) {
+    if (t < h.t || (t == h.t && idx < h.obj)) { h.t = t; h.obj = idx; h.prim = -1; }
+}
+template <int K>
+RT_DEV32 void axis_planes(CTab32& T, const RayF& r, Hit& h) {
+    if (__builtin_fabsf(comp<K>(r.d)) < 1e-4f) return;
+#pragma unroll
+    for (int j = 0; j < kMaxAxisPlanes; ++j) {
+        if (j < T.n_ax[K]) {
+            const float tt = (T.ax_pos[K][j] - comp<K>(r.o)) * comp<K>(r.inv);
+            if (tt >= 0.f) consider(h, tt, T.ax_idx[K][j]);
+        }
+    }
+}
+template <int K>
+RT_DEV32 bool axis_planes_block(CTab32& T, const RayF& r, F3 y, float lim) {
+#pragma unroll
+    for (int j = 0; j < kMaxAxisPlanes; ++j) {
+        if (j < T.n_ax[K]) {
+            const float p = T.ax_pos[K][j];
+            const float sx = comp<K>(r.o) - p, sy = comp<K>(y) - p;
+            if (!((sx > 0.f && sy > 0.f) || (sx < 0.f && sy < 0.f)) && __builtin_fabsf(comp<K>(r.d)) >= 1e-4f) {
+                const float tt = -sx * comp<K>(r.inv);
+                if (tt >= 0.f && tt < lim) return true;
+            }
+        }
+    }
+    return false;
+}
+
+template <bool MESH>
+RT_DEV32 void generic_closest(const DevScene& sc, CObj& o, int i, const RayF& r, Hit& h);
+
+// Scene::trace_ray (scene.rs:272-289): nearest over all objects, strict < in index order.
 template <bool MESH>
 RT_DEV32 Hit trace_closest(const DevScene& sc, const RayF& r) {
     Hit h{3.0e38f, -1, -1};
+    CTab32& T = tables32(sc);
+    if (T.ok) {  // compact scene: unrolled per-type tables (one scalar-load batch)
+        axis_planes<0>(T, r, h);
+        axis_planes<1>(T, r, h);
+        axis_planes<2>(T, r, h);
+#pragma unroll
+        for (int j = 0; j < kMaxSpheres; ++j) {
+            float t;
+            if (j < T.n_sph && sphere_c(T.sph[j][0], T.sph[j][1], T.sph[j][2], T.sph[j][3], r.o, r.d, &t))
+                consider(h, t, T.sph_idx[j]);
+        }
+        for (int j = 0; j < T.n_gen; ++j) {
+            const int i = T.gen_idx[j];
+            generic_closest<MESH>(sc, obj_u(sc, i), i, r, h);
+        }
+        return h;
+    }
     for (int i = 0; i < sc.n_objects; ++i) {
-        const Obj32& o = sc.obj32[i];
+        CObj& o = obj_u(sc, i);
         float t;
         if (o.geom == GEOM_SPHERE) {
             if (sphere_t(o, r.o, r.d, &t) && t < h.t) { h.t = t; h.obj = i; }
         } else if (o.geom == GEOM_PLANE) {
-            if (plane_t(o, r.o, r.d, &t) && t < h.t) { h.t = t; h.obj = i; }
+            const int ax = o.axis;
+            bool hit;
+            if (ax == 0) hit = axis_t<0>(o, r.o, r.d, r.inv, &t);
+            else if (ax == 1) hit = axis_t<1>(o, r.o, r.d, r.inv, &t);
+            else if (ax == 2) hit = axis_t<2>(o, r.o, r.d, r.inv, &t);
+            else hit = plane_t(o, r.o, r.d, &t);
+            if (hit && t < h.t) { h.t = t; h.obj = i; }
         } else if constexpr (MESH) {
             t = h.t;
             int prim = -1;
-            if (mesh_t<false>(sc, sc.meshes[o.mesh], r, &t, &prim) && t < h.t) { h.t = t; h.obj = i; h.prim = prim; }
+            if (mesh_t<false>(sc, o.mesh, r, &t, &prim) && t < h.t) { h.t = t; h.obj = i; h.prim = prim; }
         }
     }
     return h;
@@ -177,22 +296,81 @@ RT_DEV32 Hit trace_closest(const DevScene& sc, const RayF& r) {
 // Scene::mutually_visible (scene.rs:250-270) as an any-hit query: blocked iff some object's hit
 // satisfies t + 0.001 < |y - x|.
 template <bool MESH>
-RT_DEV32 bool visible(const DevScene& sc, const RayF& r, float dist) {
+RT_DEV32 bool generic_blocks(const DevScene& sc, CObj& o, const RayF& r, float lim);
+
+template <bool MESH>
+RT_DEV32 bool visible(const DevScene& sc, const RayF& r, F3 y, float dist) {
     const float lim = dist - 0.001f;
+    CTab32& T = tables32(sc);
+    if (T.ok) {
+        if (axis_planes_block<0>(T, r, y, lim) || axis_planes_block<1>(T, r, y, lim) ||
+            axis_planes_block<2>(T, r, y, lim))
+            return false;
+#pragma unroll
+        for (int j = 0; j < kMaxSpheres; ++j) {
+            float t;
+            if (j < T.n_sph && sphere_c(T.sph[j][0], T.sph[j][1], T.sph[j][2], T.sph[j][3], r.o, r.d, &t) && t < lim)
+                return false;
+        }
+        for (int j = 0; j < T.n_gen; ++j)
+            if (generic_blocks<MESH>(sc, obj_u(sc, T.gen_idx[j]), r, lim)) return false;
+        return true;
+    }
     for (int i = 0; i < sc.n_objects; ++i) {
-        const Obj32& o = sc.obj32[i];
+        CObj& o = obj_u(sc, i);
         float t;
         if (o.geom == GEOM_SPHERE) {
             if (sphere_t(o, r.o, r.d, &t) && t < lim) return false;
         } else if (o.geom == GEOM_PLANE) {
-            if (plane_t(o, r.o, r.d, &t) && t < lim) return false;
+            const int ax = o.axis;
+            if (ax == 0) {
+                if (axis_blocks<0>(o, r.o, y, r.d, r.inv, lim)) return false;
+            } else if (ax == 1) {
+                if (axis_blocks<1>(o, r.o, y, r.d, r.inv, lim)) return false;
+            } else if (ax == 2) {
+                if (axis_blocks<2>(o, r.o, y, r.d, r.inv, lim)) return false;
+            } else if (plane_t(o, r.o, r.d, &t) && t < lim) {
+                return false;
+            }
         } else if constexpr (MESH) {
             t = lim;
             int prim;
-            if (lim > 0.f && mesh_t<true>(sc, sc.meshes[o.mesh], r, &t, &prim)) return false;
+            if (lim > 0.f && mesh_t<true>(sc, o.mesh, r, &t, &prim)) return false;
         }
     }
     return true;
+}
+
+// Objects outside the compact tables: meshes and planes that are not axis-aligned.
+template <bool MESH>
+RT_DEV32 void generic_closest(const DevScene& sc, CObj& o, int i, const RayF& r, Hit& h) {
+    float t;
+    if (o.geom == GEOM_PLANE) {
+        if (plane_t(o, r.o, r.d, &t)) consider(h, t, i);
+    } else if constexpr (MESH) {
+        if (o.geom == GEOM_MESH) {
+            t = h.t;
+            int prim = -1;
+            if (mesh_t<false>(sc, o.mesh, r, &t, &prim) && (t < h.t || (t == h.t && i < h.obj))) {
+                h.t = t;
+                h.obj = i;
+                h.prim = prim;
+            }
+        }
+    }
+}
+template <bool MESH>
+RT_DEV32 bool generic_blocks(const DevScene& sc, CObj& o, const RayF& r, float lim) {
+    float t;
+    if (o.geom == GEOM_PLANE) return plane_t(o, r.o, r.d, &t) && t < lim;
+    if constexpr (MESH) {
+        if (o.geom == GEOM_MESH && lim > 0.f) {
+            t = lim;
+            int prim;
+            return mesh_t<true>(sc, o.mesh, r, &t, &prim);
+        }
+    }
+    return false;
 }
 
 enum : int { K_CAMERA = 0, K_SPEC = 1, K_DIFF = 2 };
@@ -207,7 +385,7 @@ struct Path {
 
 struct Cam {
     F3 pos, dir, cx, cy;
-    float w, h;
+    float rw, rh;  // 1 / width, 1 / height
 };
 
 // sample_pixel's camera ray (server.rs:338-357) for sample `smp` of tile subpixel `id`.
@@ -216,10 +394,10 @@ RT_DEV32 void begin_sample(const Cam& cam, const RenderArgs& a, long id, int smp
     f64::Rng rng(a.seed, sp.pid, (uint32_t)smp, (uint32_t)sp.sub);
     const float u1 = uni(rng), u2 = uni(rng);
     const float r1 = 2.f * u1, r2 = 2.f * u2;
-    const float dx = r1 < 1.f ? __builtin_sqrtf(r1) - 1.f : 1.f - __builtin_sqrtf(2.f - r1);
-    const float dy = r2 < 1.f ? __builtin_sqrtf(r2) - 1.f : 1.f - __builtin_sqrtf(2.f - r2);
-    const F3 d = cam.cx * ((((float)sp.sx + 0.5f + dx) * 0.5f + (float)sp.col) / cam.w - 0.5f) +
-                 cam.cy * ((((float)sp.sy + 0.5f + dy) * 0.5f + (float)sp.yref) / cam.h - 0.5f) + cam.dir;
+    const float dx = r1 < 1.f ? sqrt_a(r1) - 1.f : 1.f - sqrt_a(2.f - r1);
+    const float dy = r2 < 1.f ? sqrt_a(r2) - 1.f : 1.f - sqrt_a(2.f - r2);
+    const F3 d = cam.cx * ((((float)sp.sx + 0.5f + dx) * 0.5f + (float)sp.col) * cam.rw - 0.5f) +
+                 cam.cy * ((((float)sp.sy + 0.5f + dy) * 0.5f + (float)sp.yref) * cam.rh - 0.5f) + cam.dir;
     ps.ro = cam.pos;
     ps.rd = normalize(d);
     ps.r0 = rng.s0;
@@ -252,8 +430,8 @@ RT_DEV32 bool shade(const DevScene& sc, Path& ps, const Hit& h, float light_pdf)
         ps.L = ps.L + mult(ps.bemit, Le);
     } else if (MIS && h.obj == sc.light && ps.pdf_prev > 0.f) {
         const float cosl = -dot(n, ps.rd);
-        const float pdf_l = light_pdf * (h.t * h.t) / cosl;
-        ps.L = ps.L + mult(ps.beta, Le * (ps.pdf_prev / (ps.pdf_prev + pdf_l)));
+        const float pdf_l = light_pdf * (h.t * h.t) * rcp(cosl);
+        ps.L = ps.L + mult(ps.beta, Le * (ps.pdf_prev * rcp(ps.pdf_prev + pdf_l)));
     }
     if (ps.kind != K_SPEC) ps.o = -ps.rd;
     ps.depth += 1;
@@ -263,29 +441,29 @@ RT_DEV32 bool shade(const DevScene& sc, Path& ps, const Hit& h, float light_pdf)
     const F3 k = ld3f(obj.k);
     if (!spec) {
         // next-event estimation to the sphere light (scene.rs:217-229, geometry.rs:573-585)
-        const Obj32& Lo = sc.obj32[sc.light];
+        CObj& Lo = obj_u(sc, sc.light);
         const float xi1 = uni(rng), xi2 = uni(rng);
         const float z = 2.f * xi1 - 1.f;
         float sphi, cphi;
         __sincosf(6.283185307179586f * xi2, &sphi, &cphi);
-        const float sz = __builtin_sqrtf(fmaxf(0.f, 1.f - z * z));
+        const float sz = sqrt_a(fmaxf(0.f, 1.f - z * z));
         const F3 ny = f3(sz * cphi, sz * sphi, z);
-        const F3 y = ld3f(Lo.pos) + ny * Lo.r;
+        const F3 y = ld3c(Lo.pos) + ny * Lo.r;
         const F3 diff = y - x;
         const float r_sqr = dot(diff, diff);
-        const float dist = __builtin_sqrtf(r_sqr);
+        const float dist = sqrt_a(r_sqr);
         const F3 i = diff * rcp(dist);
-        const F3 lef = mult(ld3f(Lo.emitted), k) * INV_PI;
+        const F3 lef = mult(ld3c(Lo.emitted), k) * INV_PI;
         if (!is_zero(lef)) {
-            const bool vis = visible<MESH>(sc, make_ray(x, i), dist);
+            const bool vis = visible<MESH>(sc, make_ray(x, i), y, dist);
             const float cosx = dot(n, i), cosl = -dot(ny, i);
             F3 c = f3(0.f, 0.f, 0.f);
             if (!MIS) {
-                if (vis) c = lef * (cosx * cosl / (r_sqr * light_pdf));
+                if (vis) c = lef * (cosx * cosl * rcp(r_sqr * light_pdf));
             } else {
-                const float pdf_l = light_pdf * r_sqr / cosl;
+                const float pdf_l = light_pdf * r_sqr * rcp(cosl);
                 const float pdf_b = cosx * INV_PI;
-                if (vis && cosl > 0.f && pdf_b > 0.f) c = lef * (cosx / (pdf_l + pdf_b));
+                if (vis && cosl > 0.f && pdf_b > 0.f) c = lef * (cosx * rcp(pdf_l + pdf_b));
             }
             ps.L = ps.L + mult(ps.beta, c);
         }
@@ -295,8 +473,8 @@ RT_DEV32 bool shade(const DevScene& sc, Path& ps, const Hit& h, float light_pdf)
     F3 wi;
     float pdf = 0.f;
     if (!spec) {
-        const float z = __builtin_sqrtf(uni(rng));
-        const float rr = __builtin_sqrtf(fmaxf(0.f, 1.f - z * z));
+        const float z = sqrt_a(uni(rng));
+        const float rr = sqrt_a(fmaxf(0.f, 1.f - z * z));
         float sphi, cphi;
         __sincosf(6.283185307179586f * uni(rng), &sphi, &cphi);
         // create_local_coord (scene.rs:112-123)
@@ -334,16 +512,16 @@ RT_DEV32 long wave_ticket(uint32_t* counter, bool want) {
 // Persistent path loop: a resident grid whose lanes take subpixels from a global counter and walk
 // their spp/4 samples vertex by vertex (a finished sample starts the next one in the next
 // iteration). The subpixel mean is written in f64 for k_finalize_f64 (clamp, gamma, `as u8`).
-template <bool MESH, bool MIS>
-__global__ __launch_bounds__(256) void k_megakernel_f32(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
+template <bool MESH, bool MIS, int W>
+__global__ __launch_bounds__(256, W) void k_megakernel_f32(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
                                                        uint32_t* next_sub, long nsub) {
     Cam cam;
     cam.pos = f3((float)sc.cam_pos[0], (float)sc.cam_pos[1], (float)sc.cam_pos[2]);
     cam.dir = f3((float)sc.cam_dir[0], (float)sc.cam_dir[1], (float)sc.cam_dir[2]);
     cam.cx = f3((float)a.cx[0], (float)a.cx[1], (float)a.cx[2]);
     cam.cy = f3((float)a.cy[0], (float)a.cy[1], (float)a.cy[2]);
-    cam.w = (float)a.width;
-    cam.h = (float)a.height;
+    cam.rw = (float)(1.0 / a.width);
+    cam.rh = (float)(1.0 / a.height);
     const float light_pdf = (float)sc.light_pdf;
     uint32_t nverts = 0;
     long id = wave_ticket(next_sub, true);
@@ -353,14 +531,14 @@ __global__ __launch_bounds__(256) void k_megakernel_f32(DevScene sc, RenderArgs 
     Path ps;
     if (active) begin_sample(cam, a, id, 0, ps);
     while (__any(active)) {
-        bool finished = false;
+        bool finished = false, start = false;
         if (active) {
             const Hit h = trace_closest<MESH>(sc, make_ray(ps.ro, ps.rd));
             nverts += h.obj >= 0;
             if (!shade<MESH, MIS>(sc, ps, h, light_pdf)) {
                 acc = acc + ps.L;
                 if (++smp < a.n_samples) {
-                    begin_sample(cam, a, id, smp, ps);
+                    start = true;
                 } else {
                     double* o = sub_buf + (size_t)id * 3;
                     o[0] = (double)acc.x * a.inv_n;
@@ -376,11 +554,12 @@ __global__ __launch_bounds__(256) void k_megakernel_f32(DevScene sc, RenderArgs 
                 id = t;
                 smp = 0;
                 acc = f3(0.f, 0.f, 0.f);
-                begin_sample(cam, a, id, 0, ps);
+                start = true;
             } else {
                 active = false;
             }
         }
+        if (start) begin_sample(cam, a, id, smp, ps);  // one call site: next sample or next subpixel
     }
     if (a.counters) {
         unsigned long long v = nverts;
@@ -390,10 +569,10 @@ __global__ __launch_bounds__(256) void k_megakernel_f32(DevScene sc, RenderArgs 
     }
 }
 
-template <bool MESH, bool MIS>
-static hipError_t launch_k(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
+template <bool MESH, bool MIS, int W>
+static hipError_t launch_w(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
                            hipStream_t st) {
-    auto kern = k_megakernel_f32<MESH, MIS>;
+    auto kern = k_megakernel_f32<MESH, MIS, W>;
     int dev = 0, ncu = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -401,6 +580,19 @@ static hipError_t launch_k(const DevScene& sc, const RenderArgs& a, double* sub_
     const long blocks = std::max(1L, std::min((long)ncu * per_cu, (nsub + 255) / 256));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub, nsub);
     return hipGetLastError();
+}
+
+// waves/SIMD requested from the register allocator (RT_F32_WAVES overrides for A/B runs)
+template <bool MESH, bool MIS>
+static hipError_t launch_k(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
+                           hipStream_t st) {
+    static const int env = [] { const char* v = std::getenv("RT_F32_WAVES"); return v ? std::atoi(v) : 0; }();
+    // deep meshes (the unicorn's BVH walks) hide their node-load latency with more waves:
+    // 8 waves/SIMD +12% there, cubes and cornell -20% (profiles/r01h_fp32.log)
+    const int w = env ? env : (MESH && a.mesh_nodes >= 64 ? RT_F32_W_MESH : RT_F32_W);
+    if (w >= 8) return launch_w<MESH, MIS, 8>(sc, a, sub_buf, next_sub, nsub, st);
+    if (w >= 6) return launch_w<MESH, MIS, 6>(sc, a, sub_buf, next_sub, nsub, st);
+    return launch_w<MESH, MIS, 4>(sc, a, sub_buf, next_sub, nsub, st);
 }
 
 }  // namespace f32

@@ -318,6 +318,7 @@ void pack_f32(const Packed& p, std::vector<rt::Obj32>* objs, std::vector<rt::Bvh
             if (o.geom == rt::GEOM_SPHERE) grow(std::fabs(o.pos[k]) + o.r);
             else if (o.geom == rt::GEOM_PLANE && o.n[k] != 0.0) grow(o.pos[k]);
         }
+        q.axis = o.geom == rt::GEOM_PLANE ? o.axis : -1;
         q.r = (float)o.r;
         q.r2 = (float)(o.r * o.r);
         objs->push_back(q);
@@ -376,6 +377,29 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         int32_t compact = 0;
         fill_compact(p, tab.data(), &compact);
         put(blob, &o_tab, tab);
+        std::vector<rt::Compact32> tab32(1);
+        {
+            rt::Compact32& c = tab32[0];
+            std::memset(&c, 0, sizeof c);
+            const rt::CompactTab& t = tab[0];
+            c.ok = compact;
+            for (int k = 0; k < 3; ++k) {
+                c.n_ax[k] = t.n_ax[k];
+                for (int j = 0; j < rt::kMaxAxisPlanes; ++j) {
+                    c.ax_idx[k][j] = t.ax_idx[k][j];
+                    c.ax_pos[k][j] = (float)t.ax_pos[k][j];
+                }
+            }
+            c.n_sph = t.n_sph;
+            c.n_gen = t.n_gen;
+            for (int j = 0; j < rt::kMaxSpheres; ++j) {
+                c.sph_idx[j] = t.sph_idx[j];
+                for (int q = 0; q < 4; ++q) c.sph[j][q] = (float)t.sph[j][q];
+            }
+            for (int j = 0; j < rt::kMaxGeneric; ++j) c.gen_idx[j] = t.gen_idx[j];
+        }
+        size_t o_tab32;
+        put(blob, &o_tab32, tab32);
         put(blob, &o_obj, p.objects);
         put(blob, &o_mesh, p.meshes);
         put(blob, &o_kids, p.kids);
@@ -418,6 +442,7 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.bvh32 = (const rt::Bvh32*)(b + o_bvh32);
         ds.btris32 = (const rt::Tri32*)(b + o_tri32);
         ds.off32 = off32;
+        ds.ctab32 = (const rt::Compact32*)(b + o_tab32);
         ds.compact = compact;
         ds.light = s->host.light;
         ds.light_pdf = 0.0;

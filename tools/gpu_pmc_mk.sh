@@ -1,8 +1,8 @@
 #!/bin/bash
-# SQ PMC passes on one megakernel render: PSCENE="scene w h spp" (default cornell 1920x1080x64)
+# SQ PMC passes on one megakernel render: PSCENE="scene w h spp" (default cornell 1920x1080x64), PMODE=mk|f32
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-P="python tools/prof_render.py ${PSCENE:-cornell_box 1920 1080 64} mk"
+P="python tools/prof_render.py ${PSCENE:-cornell_box 1920 1080 64} ${PMODE:-mk}"
 i=0
 for C in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU" \
          "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64" \

@@ -1,4 +1,4 @@
-"""One render through the C ABI for profiling runs: python tools/prof_render.py SCENE W H SPP [mk|wf] [mis] [nearest]"""
+"""One render through the C ABI for profiling runs: python tools/prof_render.py SCENE W H SPP [mk|wf|f32] [mis] [nearest]"""
 import os
 import sys
 import time
@@ -13,7 +13,8 @@ mis = "mis" in sys.argv[6:]
 nearest = "nearest" in sys.argv[6:]  # RT_FLAG_MESH_NEAREST (BVH)
 s = rt_amd.Scene.from_toml(os.path.join(REPO, "scenes", f"{scene}.toml"))
 t = time.perf_counter()
-rgb, _, st = rt_amd.render(s, w, h, spp, megakernel=(mode == "mk"), mis=mis, mesh_nearest=nearest)
+rgb, _, st = rt_amd.render(s, w, h, spp, megakernel=(mode == "mk"), mis=mis, mesh_nearest=nearest,
+                           fp32=(mode == "f32"))
 dt = time.perf_counter() - t
 n = w * h * 4 * (spp // 4)
 print(f"{scene} {w}x{h}x{spp} {mode}{' mis' if mis else ''}{' nearest' if nearest else ''}: {dt*1e3:.1f} ms wall, {st['device_ms']:.1f} ms device, "
