@@ -27,6 +27,9 @@
 #ifndef RT_F32_W
 #define RT_F32_W 4       // waves/SIMD, analytic scenes
 #endif
+#ifndef RT_F32_REFILL
+#define RT_F32_REFILL 24  // camera-buffer refill threshold (lanes per wave)
+#endif
 #ifndef RT_F32_W_MESH
 #define RT_F32_W_MESH 8  // waves/SIMD, scenes with deep meshes
 #endif
@@ -388,20 +391,27 @@ struct Cam {
     float rw, rh;  // 1 / width, 1 / height
 };
 
-// sample_pixel's camera ray (server.rs:338-357) for sample `smp` of tile subpixel `id`.
-RT_DEV32 void begin_sample(const Cam& cam, const RenderArgs& a, long id, int smp, Path& ps) {
+// sample_pixel's camera ray (server.rs:338-357) for sample `smp` of tile subpixel `id`: its
+// direction and the sample's RNG stream after the two camera draws.
+RT_DEV32 void camera_sample(const Cam& cam, const RenderArgs& a, long id, int smp, F3& rd, uint64_t& r0,
+                            uint64_t& r1) {
     const f64::SubPixel sp = f64::subpixel_of(a, id);
     f64::Rng rng(a.seed, sp.pid, (uint32_t)smp, (uint32_t)sp.sub);
     const float u1 = uni(rng), u2 = uni(rng);
-    const float r1 = 2.f * u1, r2 = 2.f * u2;
-    const float dx = r1 < 1.f ? sqrt_a(r1) - 1.f : 1.f - sqrt_a(2.f - r1);
-    const float dy = r2 < 1.f ? sqrt_a(r2) - 1.f : 1.f - sqrt_a(2.f - r2);
+    const float r1f = 2.f * u1, r2f = 2.f * u2;
+    const float dx = r1f < 1.f ? sqrt_a(r1f) - 1.f : 1.f - sqrt_a(2.f - r1f);
+    const float dy = r2f < 1.f ? sqrt_a(r2f) - 1.f : 1.f - sqrt_a(2.f - r2f);
     const F3 d = cam.cx * ((((float)sp.sx + 0.5f + dx) * 0.5f + (float)sp.col) * cam.rw - 0.5f) +
                  cam.cy * ((((float)sp.sy + 0.5f + dy) * 0.5f + (float)sp.yref) * cam.rh - 0.5f) + cam.dir;
+    rd = normalize(d);
+    r0 = rng.s0;
+    r1 = rng.s1;
+}
+RT_DEV32 void begin_path(const Cam& cam, F3 rd, uint64_t r0, uint64_t r1, Path& ps) {
     ps.ro = cam.pos;
-    ps.rd = normalize(d);
-    ps.r0 = rng.s0;
-    ps.r1 = rng.s1;
+    ps.rd = rd;
+    ps.r0 = r0;
+    ps.r1 = r1;
     ps.beta = f3(1.f, 1.f, 1.f);
     ps.L = f3(0.f, 0.f, 0.f);
     ps.bemit = f3(0.f, 0.f, 0.f);
@@ -529,16 +539,30 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f32(DevScene sc, RenderAr
     int smp = 0;
     F3 acc = f3(0.f, 0.f, 0.f);
     Path ps;
-    if (active) begin_sample(cam, a, id, 0, ps);
+    // Camera-sample buffer (one per lane, LDS): the next sample's ray + RNG state computed ahead in
+    // a camera pass the whole wave runs once >= RT_F32_REFILL lanes have an empty slot (or some lane
+    // must start a path without one), instead of a Philox + camera pass at ~7% lane utilisation in
+    // almost every iteration. Off for the 8-wave deep-mesh kernel (its LDS holds the BVH stacks).
+    constexpr bool BUF = W <= 6;
+    __shared__ float s_cd[BUF ? 3 * 256 : 1];
+    __shared__ uint64_t s_cr[BUF ? 2 * 256 : 1];
+    bool nb = false;  // slot holds sample smp + 1 of subpixel id
+    bool start = active;
     while (__any(active)) {
-        bool finished = false, start = false;
-        if (active) {
+        bool finished = false;
+        if (active && !start) {
             const Hit h = trace_closest<MESH>(sc, make_ray(ps.ro, ps.rd));
             nverts += h.obj >= 0;
             if (!shade<MESH, MIS>(sc, ps, h, light_pdf)) {
                 acc = acc + ps.L;
                 if (++smp < a.n_samples) {
-                    start = true;
+                    if (BUF && nb) {
+                        const int l = threadIdx.x;
+                        begin_path(cam, f3(s_cd[l], s_cd[256 + l], s_cd[512 + l]), s_cr[l], s_cr[256 + l], ps);
+                        nb = false;
+                    } else {
+                        start = true;
+                    }
                 } else {
                     double* o = sub_buf + (size_t)id * 3;
                     o[0] = (double)acc.x * a.inv_n;
@@ -555,11 +579,33 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f32(DevScene sc, RenderAr
                 smp = 0;
                 acc = f3(0.f, 0.f, 0.f);
                 start = true;
+                nb = false;
             } else {
                 active = false;
             }
         }
-        if (start) begin_sample(cam, a, id, smp, ps);  // one call site: next sample or next subpixel
+        bool fill = false;
+        if constexpr (BUF) {
+            fill = active && !start && !nb && smp + 1 < a.n_samples;
+            if (!__any(start) && __popcll(__ballot(fill)) < RT_F32_REFILL) fill = false;
+        }
+        if (start || fill) {  // camera pass: paths that start now, then buffer refills
+            F3 rd;
+            uint64_t r0, r1;
+            camera_sample(cam, a, id, start ? smp : smp + 1, rd, r0, r1);
+            if (start) {
+                begin_path(cam, rd, r0, r1, ps);
+            } else {
+                const int l = threadIdx.x;
+                s_cd[l] = rd.x;
+                s_cd[256 + l] = rd.y;
+                s_cd[512 + l] = rd.z;
+                s_cr[l] = r0;
+                s_cr[256 + l] = r1;
+                nb = true;
+            }
+            start = false;
+        }
     }
     if (a.counters) {
         unsigned long long v = nverts;
