@@ -45,6 +45,7 @@ struct alignas(16) DevMesh {
     double surface_area;      // Mesh.surface_area (mesh-light pdf, geometry.rs:591)
     double total_weight;      // sum of triangle areas (WeightedIndex total)
     double cull_pad;          // near_box padding: 1e-7 * max(1, |box coordinates|)
+    int32_t btri_base, pad0, pad1, pad2;  // first of this mesh's n_tris BVH-order triangles (DevScene::btris)
 };
 
 // BVH over a mesh's triangles for the nearest-triangle mode (RT_FLAG_MESH_NEAREST), nodes in DFS

@@ -28,6 +28,7 @@ struct RenderArgs {
     unsigned long long* counters;  // optional [0] = path vertices
     const int32_t* cancel;         // optional device view of the host cancel flag (mapped memory)
     double* tail_buf;              // split-tail sample radiance (see n_whole)
+    int32_t f32_brute;             // f32 mode: meshes of <= f32_brute triangles are tested without the BVH
 };
 
 // tail_buf / tail_cap: scratch for the split tail (bytes); the launcher sizes the tail to fit it.

@@ -170,10 +170,48 @@ __shared__ int32_t s_stack32[kBvhMaxDepth * 256];
 // Nearest triangle of mesh m closer than *t (the Mesh::intersect `octree: None` loop,
 // geometry.rs:886-903, accelerated). any_hit: stop at the first triangle closer than *t.
 template <bool any_hit>
-RT_DEV32 bool mesh_t(const DevScene& sc, int mesh, const RayF& r, float* t, int* prim) {
+RT_DEV32 bool mesh_t(const DevScene& sc, int mesh, const RayF& r, float* t, int* prim, int brute) {
     typedef const __attribute__((address_space(4))) DevMesh CMesh;
     CMesh& m = ((CMesh*)sc.meshes)[__builtin_amdgcn_readfirstlane(mesh)];
     if (m.bvh_n <= 0) return false;
+    {
+        // root box from scalar loads (the root is the same node for every lane): most rays miss
+        // small meshes' boxes and skip the vector-load walk entirely
+        typedef const __attribute__((address_space(4))) Bvh32 CBvh;
+        CBvh& root = ((CBvh*)sc.bvh32)[__builtin_amdgcn_readfirstlane(m.bvh_base)];
+        Bvh32 rn;
+        for (int k = 0; k < 3; ++k) {
+            rn.bmin[k] = root.bmin[k];
+            rn.bmax[k] = root.bmax[k];
+        }
+        if (!box_hit(rn, r, *t)) return false;
+    }
+    if (m.n_tris <= brute) {
+        // small mesh (the cubes' 12 triangles): every triangle from scalar loads, no walk
+        typedef const __attribute__((address_space(4))) Tri32 CTri;
+        const int base = __builtin_amdgcn_readfirstlane(m.btri_base);
+        bool found = false;
+        float best = *t;
+        for (int j = 0; j < m.n_tris; ++j) {
+            CTri& c = ((CTri*)sc.btris32)[base + j];
+            Tri32 tr;
+            for (int k = 0; k < 3; ++k) {
+                tr.a[k] = c.a[k];
+                tr.ab[k] = c.ab[k];
+                tr.ac[k] = c.ac[k];
+                tr.n[k] = c.n[k];
+            }
+            float tt;
+            if (tri_t(tr, r.o, r.d, &tt) && tt < best) {
+                best = tt;
+                *prim = base + j;
+                found = true;
+                if (any_hit) break;
+            }
+        }
+        if (found) *t = best;
+        return found;
+    }
     __attribute__((address_space(3))) int32_t* stk = (__attribute__((address_space(3))) int32_t*)s_stack32 + threadIdx.x;
     int cur = m.bvh_base, sp = 0;
     bool found = false;
@@ -251,11 +289,11 @@ RT_DEV32 bool axis_planes_block(CTab32& T, const RayF& r, F3 y, float lim) {
 }
 
 template <bool MESH>
-RT_DEV32 void generic_closest(const DevScene& sc, CObj& o, int i, const RayF& r, Hit& h);
+RT_DEV32 void generic_closest(const DevScene& sc, CObj& o, int i, const RayF& r, Hit& h, int brute);
 
 // Scene::trace_ray (scene.rs:272-289): nearest over all objects, strict < in index order.
 template <bool MESH>
-RT_DEV32 Hit trace_closest(const DevScene& sc, const RayF& r) {
+RT_DEV32 Hit trace_closest(const DevScene& sc, const RayF& r, int brute) {
     Hit h{3.0e38f, -1, -1};
     CTab32& T = tables32(sc);
     if (T.ok) {  // compact scene: unrolled per-type tables (one scalar-load batch)
@@ -270,7 +308,7 @@ RT_DEV32 Hit trace_closest(const DevScene& sc, const RayF& r) {
         }
         for (int j = 0; j < T.n_gen; ++j) {
             const int i = T.gen_idx[j];
-            generic_closest<MESH>(sc, obj_u(sc, i), i, r, h);
+            generic_closest<MESH>(sc, obj_u(sc, i), i, r, h, brute);
         }
         return h;
     }
@@ -290,7 +328,7 @@ RT_DEV32 Hit trace_closest(const DevScene& sc, const RayF& r) {
         } else if constexpr (MESH) {
             t = h.t;
             int prim = -1;
-            if (mesh_t<false>(sc, o.mesh, r, &t, &prim) && t < h.t) { h.t = t; h.obj = i; h.prim = prim; }
+            if (mesh_t<false>(sc, o.mesh, r, &t, &prim, brute) && t < h.t) { h.t = t; h.obj = i; h.prim = prim; }
         }
     }
     return h;
@@ -299,10 +337,10 @@ RT_DEV32 Hit trace_closest(const DevScene& sc, const RayF& r) {
 // Scene::mutually_visible (scene.rs:250-270) as an any-hit query: blocked iff some object's hit
 // satisfies t + 0.001 < |y - x|.
 template <bool MESH>
-RT_DEV32 bool generic_blocks(const DevScene& sc, CObj& o, const RayF& r, float lim);
+RT_DEV32 bool generic_blocks(const DevScene& sc, CObj& o, const RayF& r, float lim, int brute);
 
 template <bool MESH>
-RT_DEV32 bool visible(const DevScene& sc, const RayF& r, F3 y, float dist) {
+RT_DEV32 bool visible(const DevScene& sc, const RayF& r, F3 y, float dist, int brute) {
     const float lim = dist - 0.001f;
     CTab32& T = tables32(sc);
     if (T.ok) {
@@ -316,7 +354,7 @@ RT_DEV32 bool visible(const DevScene& sc, const RayF& r, F3 y, float dist) {
                 return false;
         }
         for (int j = 0; j < T.n_gen; ++j)
-            if (generic_blocks<MESH>(sc, obj_u(sc, T.gen_idx[j]), r, lim)) return false;
+            if (generic_blocks<MESH>(sc, obj_u(sc, T.gen_idx[j]), r, lim, brute)) return false;
         return true;
     }
     for (int i = 0; i < sc.n_objects; ++i) {
@@ -338,7 +376,7 @@ RT_DEV32 bool visible(const DevScene& sc, const RayF& r, F3 y, float dist) {
         } else if constexpr (MESH) {
             t = lim;
             int prim;
-            if (lim > 0.f && mesh_t<true>(sc, o.mesh, r, &t, &prim)) return false;
+            if (lim > 0.f && mesh_t<true>(sc, o.mesh, r, &t, &prim, brute)) return false;
         }
     }
     return true;
@@ -346,7 +384,7 @@ RT_DEV32 bool visible(const DevScene& sc, const RayF& r, F3 y, float dist) {
 
 // Objects outside the compact tables: meshes and planes that are not axis-aligned.
 template <bool MESH>
-RT_DEV32 void generic_closest(const DevScene& sc, CObj& o, int i, const RayF& r, Hit& h) {
+RT_DEV32 void generic_closest(const DevScene& sc, CObj& o, int i, const RayF& r, Hit& h, int brute) {
     float t;
     if (o.geom == GEOM_PLANE) {
         if (plane_t(o, r.o, r.d, &t)) consider(h, t, i);
@@ -354,7 +392,7 @@ RT_DEV32 void generic_closest(const DevScene& sc, CObj& o, int i, const RayF& r,
         if (o.geom == GEOM_MESH) {
             t = h.t;
             int prim = -1;
-            if (mesh_t<false>(sc, o.mesh, r, &t, &prim) && (t < h.t || (t == h.t && i < h.obj))) {
+            if (mesh_t<false>(sc, o.mesh, r, &t, &prim, brute) && (t < h.t || (t == h.t && i < h.obj))) {
                 h.t = t;
                 h.obj = i;
                 h.prim = prim;
@@ -363,14 +401,14 @@ RT_DEV32 void generic_closest(const DevScene& sc, CObj& o, int i, const RayF& r,
     }
 }
 template <bool MESH>
-RT_DEV32 bool generic_blocks(const DevScene& sc, CObj& o, const RayF& r, float lim) {
+RT_DEV32 bool generic_blocks(const DevScene& sc, CObj& o, const RayF& r, float lim, int brute) {
     float t;
     if (o.geom == GEOM_PLANE) return plane_t(o, r.o, r.d, &t) && t < lim;
     if constexpr (MESH) {
         if (o.geom == GEOM_MESH && lim > 0.f) {
             t = lim;
             int prim;
-            return mesh_t<true>(sc, o.mesh, r, &t, &prim);
+            return mesh_t<true>(sc, o.mesh, r, &t, &prim, brute);
         }
     }
     return false;
@@ -424,7 +462,7 @@ RT_DEV32 void begin_path(const Cam& cam, F3 rd, uint64_t r0, uint64_t r1, Path& 
 // One path vertex (integrator_f64.h: shade_vertex, same walk and draw order). Returns true when the
 // path continues with ps.ro / ps.rd.
 template <bool MESH, bool MIS>
-RT_DEV32 bool shade(const DevScene& sc, Path& ps, const Hit& h, float light_pdf) {
+RT_DEV32 bool shade(const DevScene& sc, Path& ps, const Hit& h, float light_pdf, int brute) {
     if (h.obj < 0) return false;
     const Obj32& obj = sc.obj32[h.obj];
     F3 x = ps.ro + h.t * ps.rd, n;
@@ -465,7 +503,7 @@ RT_DEV32 bool shade(const DevScene& sc, Path& ps, const Hit& h, float light_pdf)
         const F3 i = diff * rcp(dist);
         const F3 lef = mult(ld3c(Lo.emitted), k) * INV_PI;
         if (!is_zero(lef)) {
-            const bool vis = visible<MESH>(sc, make_ray(x, i), y, dist);
+            const bool vis = visible<MESH>(sc, make_ray(x, i), y, dist, brute);
             const float cosx = dot(n, i), cosl = -dot(ny, i);
             F3 c = f3(0.f, 0.f, 0.f);
             if (!MIS) {
@@ -551,9 +589,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f32(DevScene sc, RenderAr
     while (__any(active)) {
         bool finished = false;
         if (active && !start) {
-            const Hit h = trace_closest<MESH>(sc, make_ray(ps.ro, ps.rd));
+            const Hit h = trace_closest<MESH>(sc, make_ray(ps.ro, ps.rd), a.f32_brute);
             nverts += h.obj >= 0;
-            if (!shade<MESH, MIS>(sc, ps, h, light_pdf)) {
+            if (!shade<MESH, MIS>(sc, ps, h, light_pdf, a.f32_brute)) {
                 acc = acc + ps.L;
                 if (++smp < a.n_samples) {
                     if (BUF && nb) {

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -211,6 +212,7 @@ void pack_scene(rt_scene* s) {
         }
         if (oc.size() > 0 && oc.kind[0]) dm.root_leaf = leaf_of[0];
         dm.bvh_base = (int32_t)p.bvh.size();
+        dm.btri_base = (int32_t)p.btris.size();
         build_bvh(p, m, dm.tri_base);
         dm.bvh_n = (int32_t)p.bvh.size() - dm.bvh_base;
         for (size_t i = 0; i < oc.size(); ++i) {
@@ -576,6 +578,8 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
                 if (ws->ensure_tail(want) != hipSuccess) (void)hipGetLastError();  // no tail split then
             }
             if (fp32) {
+                static const int brute = [] { const char* v = std::getenv("RT_F32_BRUTE"); return v ? std::atoi(v) : 16; }();
+                a.f32_brute = brute;
                 e = rt::launch_megakernel_f32(ds, a, sub, (uint32_t*)(ws->counters + 4), st);
             } else {
                 e = rt::launch_megakernel_f64(ds, a, sub, (uint32_t*)(ws->counters + 4), ws->tail_buf, ws->tail_cap, st);
