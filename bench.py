@@ -234,7 +234,7 @@ def main():
         }
         # The megakernel's own bound is VALU issue: PMC instructions per vertex x the
         # vertex rate of this run, against 1024 SIMDs x one wave-instruction per 4 cycles at 2.4 GHz
-        valu = load_valu(f"{args.scene} megakernel") if mode == "megakernel" else None
+        valu = load_valu(f"{args.scene} {mode}") if mode.startswith("megakernel") else None
         if valu:
             rate = valu["valu_inst_per_vertex"] * st["vertices"] / (dev_ms / 1e3)
             peak = 1024 * 2.4e9 / 4

@@ -174,9 +174,9 @@ RT_DEV32 bool mesh_t(const DevScene& sc, int mesh, const RayF& r, float* t, int*
     typedef const __attribute__((address_space(4))) DevMesh CMesh;
     CMesh& m = ((CMesh*)sc.meshes)[__builtin_amdgcn_readfirstlane(mesh)];
     if (m.bvh_n <= 0) return false;
-    {
-        // root box from scalar loads (the root is the same node for every lane): most rays miss
-        // small meshes' boxes and skip the vector-load walk entirely
+    if (m.n_tris <= brute) {
+        // small mesh (the cubes' 12 triangles): root box, then every triangle, from scalar loads
+        // (the same data for every lane); most rays miss the box
         typedef const __attribute__((address_space(4))) Bvh32 CBvh;
         CBvh& root = ((CBvh*)sc.bvh32)[__builtin_amdgcn_readfirstlane(m.bvh_base)];
         Bvh32 rn;
@@ -185,9 +185,6 @@ RT_DEV32 bool mesh_t(const DevScene& sc, int mesh, const RayF& r, float* t, int*
             rn.bmax[k] = root.bmax[k];
         }
         if (!box_hit(rn, r, *t)) return false;
-    }
-    if (m.n_tris <= brute) {
-        // small mesh (the cubes' 12 triangles): every triangle from scalar loads, no walk
         typedef const __attribute__((address_space(4))) Tri32 CTri;
         const int base = __builtin_amdgcn_readfirstlane(m.btri_base);
         bool found = false;
