@@ -48,7 +48,9 @@ extern "C" {
 /* rt_render_params.flags */
 #define RT_FLAG_MIS (1u << 0)        /* config.toml `use_mis` (dead in the reference, scene.rs:188): build-defined balance heuristic */
 #define RT_FLAG_MEGAKERNEL (1u << 1) /* fused per-lane path loop instead of the wavefront pipeline */
-#define RT_FLAG_FP32 (1u << 2)       /* f32 arithmetic (statistical parity only); default is the reference's f64 */
+#define RT_FLAG_FP32 (1u << 2)       /* f32 perf mode (statistical parity only): diffuse/mirror BRDFs and
+                                        sphere lights (RT_E_INVAL otherwise), meshes with nearest-triangle semantics;
+                                        implies the megakernel. Default is the reference's f64 */
 #define RT_FLAG_MESH_NEAREST (1u << 3) /* Mesh::intersect's `octree: None` branch (geometry.rs:886-903: nearest
                                           triangle, strict < in index order) instead of the octree walk, accelerated on
                                           the device by a BVH; megakernel only (RT_E_INVAL with the wavefront) */
