@@ -301,3 +301,24 @@ def test_fp32_rejects_unsupported(rt, gpu_scenes):
     with pytest.raises(rt.RtError):
         rt.render(phong, 8, 8, 4, SEED, fp32=True)
     rt.render(phong, 8, 8, 4, SEED)  # the f64 path renders it
+
+
+def test_fp32_cancel_and_tiling(rt, gpu_scenes):
+    """The f32 kernel polls the cancel flag like the f64 megakernel, and its frame does not depend on
+    the tiling (the RNG is keyed by global pixel, sample and subpixel)."""
+    import ctypes
+    import threading
+    import time
+
+    flag = ctypes.c_int32(0)
+    timer = threading.Timer(0.3, lambda: setattr(flag, "value", 1))
+    t0 = time.time()
+    timer.start()
+    _, _, st = rt.render(gpu_scenes["cornell_box"], 1920, 1080, 8192, SEED, fp32=True, cancel=flag)
+    dt = time.time() - t0
+    timer.cancel()
+    assert st["cancelled"] and dt < 4.0, (st["cancelled"], dt)
+    sc = gpu_scenes["cubes"]
+    full, sub_full, _ = rt.render(sc, 96, 64, 8, SEED, fp32=True, want_sub=True)
+    tile, sub_tile, _ = rt.render(sc, 96, 64, 8, SEED, tile=(32, 16, 40, 24), fp32=True, want_sub=True)
+    assert np.array_equal(tile, full[16:40, 32:72]) and np.array_equal(sub_tile, sub_full[16:40, 32:72])
