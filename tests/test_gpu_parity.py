@@ -322,3 +322,24 @@ def test_fp32_cancel_and_tiling(rt, gpu_scenes):
     full, sub_full, _ = rt.render(sc, 96, 64, 8, SEED, fp32=True, want_sub=True)
     tile, sub_tile, _ = rt.render(sc, 96, 64, 8, SEED, tile=(32, 16, 40, 24), fp32=True, want_sub=True)
     assert np.array_equal(tile, full[16:40, 32:72]) and np.array_equal(sub_tile, sub_full[16:40, 32:72])
+
+
+@pytest.mark.parametrize("asset", ["chair.obj", "crewmate.obj"])
+def test_extra_assets_parity(asset, rt, oracle, tmp_path):
+    """The reference's other OBJ assets in a room: f64 megakernel and wavefront
+    against the oracle (1e-9 / RGB8 bounds of §8c.1), and the f32 mode against the f64
+    nearest-triangle path (§8c.2 bounds)."""
+    from test_host_prep import extra_asset_scene
+
+    p = extra_asset_scene(tmp_path, asset)
+    sc, orc = rt.Scene.from_toml(p), oracle.OracleScene(p)
+    w, h, spp = 64, 48, 8
+    rgb_o, sub_o, st_o = orc.render(w, h, spp, SEED)
+    for mk in (True, False):
+        rgb_g, sub_g, st = rt.render(sc, w, h, spp, SEED, megakernel=mk, want_sub=True)
+        assert 0.9 * st_o["vertices"] <= st["vertices"] <= st_o["vertices"]
+        _assert_parity(rgb_g, sub_g, rgb_o, sub_o, f"{asset}/{'mk' if mk else 'wf'}")
+    w, h, spp = 128, 96, 64
+    rgb_f, sub_f, _ = rt.render(sc, w, h, spp, SEED, want_sub=True, fp32=True)
+    rgb_d, sub_d, _ = rt.render(sc, w, h, spp, SEED, want_sub=True, megakernel=True, mesh_nearest=True)
+    _assert_fp32_stats(sub_f, sub_d, rgb_f, rgb_d, f"{asset}/f32")

@@ -165,3 +165,66 @@ def test_root_order_sorting_network():
     for _ in range(20000):
         keys = [rnd.choice([0.5, 1.0, 2.0, rnd.random()]) for _ in range(8)]
         assert network(keys) == insertion(keys)
+
+
+EXTRA_ASSET_SCENE = """
+[camera]
+pos = [50.0, 52.0, 295.6]
+dir = [0.0, -0.042612, -1.0]
+[[objects]]
+brdf = {{ type = "diffuse", kd = [0.75, 0.25, 0.25] }}
+geometry = {{ type = "plane", pos = [1.0, 0.0, 0.0], n = [1.0, 0.0, 0.0] }}
+[[objects]]
+brdf = {{ type = "diffuse", kd = [0.25, 0.25, 0.75] }}
+geometry = {{ type = "plane", pos = [99.0, 0.0, 0.0], n = [-1.0, 0.0, 0.0] }}
+[[objects]]
+brdf = {{ type = "diffuse", kd = [0.75, 0.75, 0.75] }}
+geometry = {{ type = "plane", pos = [0.0, 0.0, 0.0], n = [0.0, 1.0, 0.0] }}
+[[objects]]
+brdf = {{ type = "diffuse", kd = [0.75, 0.75, 0.75] }}
+geometry = {{ type = "plane", pos = [0.0, 81.6, 0.0], n = [0.0, -1.0, 0.0] }}
+[[objects]]
+brdf = {{ type = "diffuse", kd = [0.75, 0.75, 0.75] }}
+geometry = {{ type = "plane", pos = [0.0, 0.0, 0.0], n = [0.0, 0.0, 1.0] }}
+[[objects]]
+brdf = {{ type = "diffuse", kd = [0.8, 0.7, 0.5] }}
+geometry = {{ type = "mesh", path = "{asset}" }}
+transforms = [
+    {{ scale = {scale} }},
+    {{ rotate_y = 0.6 }},
+    {{ translate = [50.0, {ty}, 70.0] }},
+]
+[[objects]]
+emitted = [50.0, 50.0, 50.0]
+brdf = {{ type = "diffuse", kd = [0.0, 0.0, 0.0] }}
+geometry = {{ type = "sphere", pos = [50.0, 70.0, 100.0], r = 4.0 }}
+"""
+
+
+def extra_asset_scene(tmp_path, asset):
+    """A room around one of the reference's unused assets (scenes/assets/chair.obj, crewmate.obj:
+    `v/vt/vn` faces, Blender exports)."""
+    scale, ty = {"chair.obj": (30.0, 24.5), "crewmate.obj": (0.25, -73.7)}[asset]
+    d = tmp_path / asset.split(".")[0]
+    d.mkdir()
+    os.symlink(os.path.join(REPO, "scenes", "assets"), d / "assets")
+    p = d / "s.toml"
+    p.write_text(EXTRA_ASSET_SCENE.format(asset=asset, scale=scale, ty=ty))
+    return str(p)
+
+
+@pytest.mark.parametrize("asset", ["chair.obj", "crewmate.obj"])
+def test_extra_assets_prep_matches_oracle(asset, rt, oracle, tmp_path):
+    """the reference's other OBJ assets load through the product's host prep
+    exactly as through the oracle's restatement of Mesh::load + Octree::build."""
+    p = extra_asset_scene(tmp_path, asset)
+    s = rt.Scene.from_toml(p)
+    o = oracle.OracleScene(p)
+    m = s.mesh(5)
+    kind_o, child_o, off_o, cnt_o, refs_o = o.mesh_octree(5)
+    verts_o, idx_o = o.mesh_vertices(5)
+    assert len(idx_o) > 100
+    assert np.array_equal(m["vertices"], verts_o)
+    assert np.array_equal(m["indices"].astype(np.int64), idx_o.astype(np.int64))
+    assert np.array_equal(m["kind"], kind_o) and np.array_equal(m["child"], child_o)
+    assert np.array_equal(m["leaf_cnt"], cnt_o) and np.array_equal(m["refs"], refs_o)
