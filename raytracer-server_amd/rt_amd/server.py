@@ -39,13 +39,14 @@ def chunk_messages(rgb, y0):
             yield struct.pack("<BBHH", 0, n, x, y0 + r) + rgb[r, x:x + n].tobytes()
 
 
-def gpu_band_renderer(device=0):
-    """Default band renderer: rt_render on `device` for rows [y0, y0 + rows)."""
+def gpu_band_renderer(device=0, fp32=False):
+    """Default band renderer: rt_render on `device` for rows [y0, y0 + rows). fp32: the f32 perf mode
+    (RT_FLAG_FP32, statistical parity only) — server-wide, the protocol is unchanged."""
     import rt_amd
 
     def render(scene, width, height, spp, seed, y0, rows, cancel):
         rgb, _, st = rt_amd.render(scene, width, height, spp, seed, tile=(0, y0, width, rows),
-                                   megakernel=True, device=device, cancel=cancel)
+                                   megakernel=True, device=device, cancel=cancel, fp32=fp32)
         return None if st["cancelled"] else rgb
 
     return render
@@ -171,7 +172,8 @@ def main(argv=None):
     scenes = {n: rt_amd.Scene.from_toml(os.path.join(scene_dir, f"{n}.toml")) for n in SCENE_NAMES}
     port = int(os.environ.get("PORT", "8080"))  # main.rs:38
     print(f"Listening on port {port}.")
-    web.run_app(Server(scenes).app(), host="0.0.0.0", port=port, print=None)
+    fp32 = os.environ.get("RT_PRECISION", "f64") == "f32"  # f64 (the reference's arithmetic) by default
+    web.run_app(Server(scenes, renderer=gpu_band_renderer(fp32=fp32)).app(), host="0.0.0.0", port=port, print=None)
     return 0
 
 
