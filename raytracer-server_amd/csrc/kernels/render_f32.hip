@@ -13,7 +13,11 @@
 //   * diffuse and mirror throughput updates in closed form (kd / p, ks / p: the f cos / (pdf p) of
 //     scene.rs:176-184 / :232-240 with pdf and cos cancelled);
 //   * meshes are intersected with nearest-triangle semantics (geometry.rs:886-903, the
-//     RT_FLAG_MESH_NEAREST branch) through the BVH with f32 boxes rounded outward.
+//     RT_FLAG_MESH_NEAREST branch): through the BVH with f32 boxes rounded outward, or, for meshes
+//     of <= RenderArgs::f32_brute triangles, triangle by triangle from scalar loads.
+// Layout of the work: a persistent resident grid, lanes pulling subpixels from one counter
+// (wave-aggregated tickets); object loops over the scalar-loaded compact tables (Compact32);
+// camera samples computed ahead into an LDS buffer in whole-wave passes.
 // Supported: diffuse and mirror BRDFs, sphere lights, spheres / planes / meshes, MIS on or off —
 // every reference scene. Phong and mesh lights are rejected on the host (rt_api.cpp).
 #include <hip/hip_runtime.h>
