@@ -85,6 +85,14 @@ void cp3(double* dst, const rt::host::D3& v) {
 // centroids along the longest axis, leaves of <= 4 triangles (or at depth kBvhMaxDepth - 1), nodes
 // in DFS pre-order (DevBvhNode). Node boxes are the triangles' vertex bounds; the traversal's slab test pads
 // them (near_box, DevMesh::cull_pad), so a triangle the ray hits is never culled.
+// RT_BVH_SAH=0 selects the median-split build (A/B); default: binned SAH.
+constexpr int kBins = 16;      // SAH bins per axis
+constexpr int kSahDepth = 16;  // deeper BVH nodes split at the median (depth stays <= kBvhMaxDepth)
+bool bvh_sah_enabled() {
+    const char* v = std::getenv("RT_BVH_SAH");
+    return !(v && std::atoi(v) == 0);
+}
+
 void build_bvh(Packed& p, const rt::host::Mesh& m, int32_t tri_base) {
     using rt::host::D3;
     struct Item { double lo[3], hi[3], c[3]; int32_t id; };
@@ -107,6 +115,64 @@ void build_bvh(Packed& p, const rt::host::Mesh& m, int32_t tri_base) {
         Packed& p;
         std::vector<Item>& it;
         int32_t tri_base;
+        bool sah;
+        // Binned surface-area heuristic (16 bins per axis over the centroid bounds): the split
+        // minimising area(L) * n(L) + area(R) * n(R); items are partitioned in place (left = lower
+        // centroids along *ax). *mid = b when no split separates the items.
+        static double half_area(const double* lo, const double* hi) {
+            const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+            return dx * dy + dy * dz + dz * dx;
+        }
+        void sah_split(size_t b, size_t e, const double* clo, const double* chi, int* ax_out, size_t* mid) {
+            double best = INFINITY;
+            int best_ax = -1, best_bin = -1;
+            for (int ax = 0; ax < 3; ++ax) {
+                const double ext = chi[ax] - clo[ax];
+                if (!(ext > 0.0)) continue;
+                double lo[kBins][3], hi[kBins][3];
+                size_t cnt[kBins] = {0};
+                for (int q = 0; q < kBins; ++q)
+                    for (int k = 0; k < 3; ++k) { lo[q][k] = INFINITY; hi[q][k] = -INFINITY; }
+                for (size_t i = b; i < e; ++i) {
+                    int q = (int)((it[i].c[ax] - clo[ax]) / ext * kBins);
+                    q = std::min(kBins - 1, std::max(0, q));
+                    ++cnt[q];
+                    for (int k = 0; k < 3; ++k) {
+                        lo[q][k] = std::min(lo[q][k], it[i].lo[k]);
+                        hi[q][k] = std::max(hi[q][k], it[i].hi[k]);
+                    }
+                }
+                double ra[kBins];
+                size_t rc[kBins];
+                double al[3] = {INFINITY, INFINITY, INFINITY}, ah[3] = {-INFINITY, -INFINITY, -INFINITY};
+                size_t ac = 0;
+                for (int q = kBins - 1; q > 0; --q) {  // suffix boxes: bins q..15
+                    for (int k = 0; k < 3; ++k) { al[k] = std::min(al[k], lo[q][k]); ah[k] = std::max(ah[k], hi[q][k]); }
+                    ac += cnt[q];
+                    rc[q] = ac;
+                    ra[q] = ac ? half_area(al, ah) : 0.0;
+                }
+                double pl[3] = {INFINITY, INFINITY, INFINITY}, ph[3] = {-INFINITY, -INFINITY, -INFINITY};
+                size_t pc = 0;
+                for (int q = 1; q < kBins; ++q) {  // split between bins q-1 and q
+                    for (int k = 0; k < 3; ++k) { pl[k] = std::min(pl[k], lo[q - 1][k]); ph[k] = std::max(ph[k], hi[q - 1][k]); }
+                    pc += cnt[q - 1];
+                    if (pc == 0 || rc[q] == 0) continue;
+                    const double cost = half_area(pl, ph) * (double)pc + ra[q] * (double)rc[q];
+                    if (cost < best) { best = cost; best_ax = ax; best_bin = q; }
+                }
+            }
+            *mid = b;
+            if (best_ax < 0) return;
+            const int ax = best_ax;
+            const double ext = chi[ax] - clo[ax];
+            auto left = [&](const Item& x) {
+                int q = (int)((x.c[ax] - clo[ax]) / ext * kBins);
+                return std::min(kBins - 1, std::max(0, q)) < best_bin;
+            };
+            *mid = (size_t)(std::stable_partition(it.begin() + b, it.begin() + e, left) - it.begin());
+            *ax_out = ax;
+        }
         void build(size_t b, size_t e, int depth) {
             const size_t node = p.bvh.size();
             p.bvh.push_back(rt::DevBvhNode{});
@@ -133,11 +199,16 @@ void build_bvh(Packed& p, const rt::host::Mesh& m, int32_t tri_base) {
                 }
             } else {
                 int ax = 0;
-                for (int k = 1; k < 3; ++k)
-                    if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
-                const size_t mid = (b + e) / 2;
-                std::nth_element(it.begin() + b, it.begin() + mid, it.begin() + e,
-                                 [ax](const Item& x, const Item& y) { return x.c[ax] < y.c[ax] || (x.c[ax] == y.c[ax] && x.id < y.id); });
+                size_t mid = 0;
+                if (sah && depth < kSahDepth) sah_split(b, e, clo, chi, &ax, &mid);
+                if (mid <= b || mid >= e) {  // median split (no SAH split found, or deep nodes)
+                    ax = 0;
+                    for (int k = 1; k < 3; ++k)
+                        if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
+                    mid = (b + e) / 2;
+                    std::nth_element(it.begin() + b, it.begin() + mid, it.begin() + e,
+                                     [ax](const Item& x, const Item& y) { return x.c[ax] < y.c[ax] || (x.c[ax] == y.c[ax] && x.id < y.id); });
+                }
                 nd.axis = ax;
                 build(b, mid, depth + 1);
                 nd.a = (int32_t)p.bvh.size();  // global index of the right child
@@ -145,7 +216,7 @@ void build_bvh(Packed& p, const rt::host::Mesh& m, int32_t tri_base) {
             }
             p.bvh[node] = nd;
         }
-    } rec{p, it, tri_base};
+    } rec{p, it, tri_base, bvh_sah_enabled()};
     if (n > 0) rec.build(0, n, 0);
 }
 
