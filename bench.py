@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=120)
     ap.add_argument("--cpu-spp", type=int, default=256)
+    ap.add_argument("--cpu-rows-1t", type=int, default=4, help="rows of the one-thread CPU sample")
     ap.add_argument("--partition", choices=["interleave", "stripes"], default="interleave")
     return ap.parse_args()
 
@@ -92,9 +93,19 @@ def cpu_baseline(args):
                          mis=args.mis, threads=threads, want_sub=False)
     dt = time.perf_counter() - t0
     samples = args.width * rows * 4 * (args.cpu_spp // 4)
+    # SURVEY §8(d) also asks for one thread: the reference renders a job on one task (server.rs:157-199)
+    rows1 = min(args.cpu_rows_1t, args.height)
+    y1 = (args.height - rows1) // 2
+    t1 = time.perf_counter()
+    sc.render(args.width, args.height, args.cpu_spp, args.seed, tile=(0, y1, args.width, rows1), mis=args.mis,
+              threads=1, want_sub=False)
+    dt1 = time.perf_counter() - t1
+    samples1 = args.width * rows1 * 4 * (args.cpu_spp // 4)
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"{args.scene} rows {y0}..{y0 + rows} of {args.width}x{args.height} at {args.cpu_spp} spp "
-                      f"({samples} samples, {dt:.1f} s, f64, CPU oracle restating server.rs:320-368 + scene.rs + geometry.rs)"}
+                      f"({samples} samples, {dt:.1f} s, f64, CPU oracle restating server.rs:320-368 + scene.rs + geometry.rs)",
+            "single_thread": {"value": samples1 / dt1 / 1e6, "cores": 1,
+                              "sample": f"rows {y1}..{y1 + rows1} at {args.cpu_spp} spp ({samples1} samples, {dt1:.1f} s)"}}
 
 
 def load_valu(workload_key):
