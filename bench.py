@@ -2,35 +2,53 @@
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1 launched by
 torch.distributed.run, one rank per GPU. A step = one full render of the frame (scene resident in
-HBM; output RGB8 gathered to rank 0). Rank r renders the interleaved rows r, r+N, r+2N, ... of the
-frame (rt_render_params.row_step = N: every rank gets the same mix of cheap and expensive rows;
---partition stripes gives contiguous stripes instead); no collective on the data path except the
-final RGB8 gather the north_star prescribes. Total work is fixed: scaling = "strong". Rank 0
-prints one JSON line.
+HBM) with the RGB8 rows copied to the host and gathered to rank 0 there: rank r renders the
+interleaved rows r, r+N, r+2N, ... of the frame (rt_render_params.row_step = N: every rank gets the
+same mix of cheap and expensive rows; --partition stripes gives contiguous stripes). The process
+group is gloo (host): the gather, the barriers and the max-over-ranks timing run over it, so no
+RCCL collective is on the data path (north_star: "tiles gathered on the host"). Total work is
+fixed: scaling = "strong". Rank 0 prints one JSON line.
 
-roofline: dominant kernel = the render kernel(s). Algorithmic bytes follow SURVEY §8(d)'s canonical
-SoA wavefront model, 88 B per camera sample + 280 B per path vertex, with the vertex count taken
-from the device counter of the same workload; achieved = those bytes / device time measured with
-HIP events on the stream the kernels run on. peak = 8.0 TB/s (MI355X HBM3E). traffic = PMC-derived
-HBM bytes per launch from profiles/ (null when not collected for this mode).
+roofline (dominant kernel = the render megakernel; kernel_ms = its average device time per launch,
+HIP events recorded on the stream the kernel runs on):
+  * bound "hbm": achieved = the HBM bytes the PMC counters measured for one launch of this exact
+    workload (profiles/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE, separate rocprofv3 passes over
+    `bench.py --steps 1 --warmup 0`, tools/gpu_task.sh benchpmc) / kernel_ms; peak 8.0 TB/s;
+    traffic = those bytes; null when no measurement exists for the workload;
+  * algorithmic_bytes_per_launch = the megakernel's own unavoidable traffic: the f64 subpixel means
+    written (4 x 3 x 8 B per pixel) and read back by the finalize, plus the RGB8 frame;
+  * wavefront_equiv_frac = SURVEY §8(d)'s canonical model (88 B per camera sample + 280 B per path
+    vertex of an f32 SoA wavefront) over kernel_ms / 8 TB/s: what the same throughput would stream
+    as a wavefront — a model, not a measurement;
+  * compute = the kernel's real bound, f64 VALU issue: the PMC instruction mix per path vertex of
+    this scene and mode (profiles/pmc_valu.json, tools/pmc_report.py) priced per class on a SIMD-32
+    (f64 add/mul/fma 4 cycles per wave64 instruction, f64 transcendental 8, 64-bit integer 4, other
+    VALU 2) times this run's vertex rate, over 1024 SIMDs x the PMC-measured clock; and the FP64
+    FLOP rate against 78.6 TFLOP/s.
 
-cpu_baseline: the CPU oracle (a line-by-line f64 restatement of the reference's sample loop, the
-reference itself is Rust and cannot be built here) on a bounded row band of the same frame, on
-min(16, cpu_count) threads, rank 0 at N = 1 only.
+cpu_baseline: the CPU oracle (a line-by-line f64 restatement of the reference's sample loop; the
+reference itself is Rust and cannot be built here), compiled on this host with -O3 -march=native,
+on a bounded row band of the same frame on min(16, cpu_count) threads, and on 1 thread; rank 0 at
+N = 1 only.
 """
 import argparse
-import ctypes
+import hashlib
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "raytracer-server_amd"))
 
 HBM_PEAK_GBS = 8000.0
+FP64_PEAK_TFLOPS = 78.6
+N_SIMD = 1024
 BYTES_PER_SAMPLE = 88
 BYTES_PER_VERTEX = 280
+VALU_COST = {"f64": 4, "trans_f64": 8, "int64": 4, "other": 2}  # cycles per wave64 instruction on a SIMD-32
 
 
 def parse():
@@ -80,7 +98,23 @@ def assemble(parts, world, height, mode="interleave"):
     return frame
 
 
+def native_oracle():
+    """The CPU oracle built for this host's CPU (-O3 -march=native); falls back to the
+    portable build if the compiler is missing."""
+    out = os.path.join(tempfile.gettempdir(), f"rt_liboracle_native_{os.getpid()}.so")
+    cmd = ["g++", "-O3", "-march=native", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-shared",
+           "-o", out, os.path.join(REPO, "oracle", "oracle.cpp"), "-lpthread"]
+    try:
+        subprocess.run(cmd, check=True, capture_output=True, timeout=120)
+        return out, "-O3 -march=native"
+    except (OSError, subprocess.SubprocessError):
+        return None, "-O3 (portable build; -march=native compile failed)"
+
+
 def cpu_baseline(args):
+    lib, flags = native_oracle()
+    if lib:
+        os.environ["RT_ORACLE_LIB"] = lib
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_bind
 
@@ -101,35 +135,41 @@ def cpu_baseline(args):
               threads=1, want_sub=False)
     dt1 = time.perf_counter() - t1
     samples1 = args.width * rows1 * 4 * (args.cpu_spp // 4)
+    if lib:
+        os.unlink(lib)
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"{args.scene} rows {y0}..{y0 + rows} of {args.width}x{args.height} at {args.cpu_spp} spp "
-                      f"({samples} samples, {dt:.1f} s, f64, CPU oracle restating server.rs:320-368 + scene.rs + geometry.rs)",
+                      f"({samples} samples, {dt:.1f} s, f64, CPU oracle restating server.rs:320-368 + scene.rs + "
+                      f"geometry.rs, g++ {flags})",
             "single_thread": {"value": samples1 / dt1 / 1e6, "cores": 1,
                               "sample": f"rows {y1}..{y1 + rows1} at {args.cpu_spp} spp ({samples1} samples, {dt1:.1f} s)"}}
 
 
-def load_valu(workload_key):
-    """VALU wave-instructions per path vertex of the dominant kernel, from the SQ PMC passes in
-    profiles/ (tools/gpu_pmc_mk.sh -> profiles/pmc_valu.json), or None."""
-    path = os.path.join(REPO, "profiles", "pmc_valu.json")
+def load_profile(name, key):
     try:
-        with open(path) as f:
-            return json.load(f).get(workload_key)
+        with open(os.path.join(REPO, "profiles", name)) as f:
+            return json.load(f).get(key)
     except (OSError, ValueError):
         return None
 
 
-def load_traffic(workload_key):
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            return json.load(f).get(workload_key)
-    except (OSError, ValueError):
-        return None
+def compute_block(mix, vertices, kernel_ms):
+    """f64 VALU issue occupancy and FP64 FLOP rate of this run from the PMC mix per path vertex."""
+    rate = vertices / (kernel_ms / 1e3)  # path vertices per second
+    cyc = sum(mix["per_vertex"][c] * VALU_COST[c] for c in VALU_COST) * rate
+    clock = mix["clock_GHz"] * 1e9
+    flops = mix["fp64_flops_per_vertex"] * rate
+    return {"bound": "valu_issue_f64", "issue_frac": round(cyc / (N_SIMD * clock), 4),
+            "issue_cycles_per_s": round(cyc, 1), "clock_GHz": mix["clock_GHz"],
+            "valu_inst_per_vertex": round(sum(mix["per_vertex"].values()), 2),
+            "fp64_tflops": round(flops / 1e12, 3), "fp64_peak_tflops": FP64_PEAK_TFLOPS,
+            "fp64_frac": round(flops / 1e12 / FP64_PEAK_TFLOPS, 4), "lane_utilisation": mix["lane_utilisation"],
+            "cost_cycles": VALU_COST, "source": mix["source"]}
 
 
 def main():
     args = parse()
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -138,7 +178,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")  # host gather + barriers; no RCCL on the data path
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
@@ -153,67 +193,74 @@ def main():
                                 row_step)
     max_rows = max(partition(r, world, args.height, args.partition)[1] for r in range(world))
     rgb = torch.zeros((max_rows, args.width, 3), dtype=torch.uint8, device="cuda")
+    host = torch.zeros((max_rows, args.width, 3), dtype=torch.uint8).pin_memory()
     stream = torch.cuda.current_stream()
-    gathered = [torch.empty_like(rgb) for _ in range(world)] if (world > 1 and rank == 0) else None
+    gathered = [torch.empty_like(host) for _ in range(world)] if (world > 1 and rank == 0) else None
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    kernel_ms = []
 
-    def step():
+    def step(timed):
+        if timed:
+            ev0.record(stream)
         rt_amd.render_device(scene, params, rgb.data_ptr(), None, stream.cuda_stream)
+        if timed:
+            ev1.record(stream)
+        host.copy_(rgb, non_blocking=True)  # the rank's rows to the host
+        stream.synchronize()
+        if timed:
+            kernel_ms.append(ev0.elapsed_time(ev1))
         if world > 1:
-            dist.gather(rgb, gathered if rank == 0 else None, dst=0)
+            dist.gather(host, gathered if rank == 0 else None, dst=0)  # host-side gather (gloo)
 
     # one untimed stats run: path-vertex count of this exact workload (device counter)
     st = rt_amd.render_device(scene, params, rgb.data_ptr(), None, stream.cuda_stream, stats=True)
     for _ in range(args.warmup):
-        step()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+        step(False)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ev0.record(stream)
     for _ in range(args.steps):
-        step()
-    ev1.record(stream)
+        step(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    t1 = time.perf_counter()
-    wall = t1 - t0
-    dev_ms = ev0.elapsed_time(ev1) / max(1, args.steps)
+    wall = time.perf_counter() - t0
+    dev_ms = sum(kernel_ms) / max(1, len(kernel_ms))
     if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
-        v = torch.tensor([st["vertices"]], dtype=torch.int64, device="cuda")
+        v = torch.tensor([st["vertices"]], dtype=torch.int64)
         dist.all_reduce(v)
         total_vertices = int(v.item())
     else:
         total_vertices = st["vertices"]
-
-    # the frame (rank 0): the gathered row sets put back in order; its digest is the same at every N
-    import hashlib
-
-    if rank == 0:
-        if world > 1:
-            frame = assemble([g.cpu().numpy() for g in gathered], world, args.height, args.partition)
-        else:
-            frame = rgb[:th].cpu().numpy()
-        digest = hashlib.sha1(frame.tobytes()).hexdigest()[:16]
 
     n_samples = args.width * args.height * 4 * (args.spp // 4)
     ms_per_step = wall * 1000.0 / args.steps
     value = n_samples / (wall / args.steps) / 1e6
 
     if rank == 0:
+        # the frame: the gathered row sets put back in order; its digest is the same at every N
+        if world > 1:
+            frame = assemble([g.numpy() for g in gathered], world, args.height, args.partition)
+        else:
+            frame = host[:th].numpy()
+        digest = hashlib.sha1(np.ascontiguousarray(frame).tobytes()).hexdigest()[:16]
         rank_samples = args.width * th * 4 * (args.spp // 4)
-        alg_bytes = BYTES_PER_SAMPLE * rank_samples + BYTES_PER_VERTEX * st["vertices"]
-        achieved = alg_bytes / (dev_ms / 1e3) / 1e9
         workload = f"{args.scene} {args.width}x{args.height}x{args.spp}spp{' mis' if args.mis else ''}"
         mode = args.mode + ("-f32" if args.fp32 else "")
         kernel = "k_megakernel_f32" if args.fp32 else (
             "k_megakernel_f64" if args.mode == "megakernel" else "k_wf_extend+k_wf_shade")
-        traffic = load_traffic(f"{workload} {mode}")
+        # traffic was measured at N = 1 on the whole frame: scale to this rank's share of the rows
+        traffic_full = load_profile("pmc_traffic.json", f"{workload} {mode}")
+        traffic = int(traffic_full * th / args.height) if traffic_full else None
+        achieved = traffic / (dev_ms / 1e3) / 1e9 if traffic else None
+        model_bytes = BYTES_PER_SAMPLE * rank_samples + BYTES_PER_VERTEX * st["vertices"]
+        npix = args.width * th
+        alg_bytes = npix * (2 * 12 * 8 + 3)  # f64 subpixel means written + read by the finalize, RGB8 out
         out = {
             "metric": "Msamples/sec (pixels x spp), cornell_box 1920x1080x1024spp" if args.scene == "cornell_box"
             and args.width == 1920 and args.height == 1080 and args.spp == 1024 and not args.fp32
@@ -233,29 +280,31 @@ def main():
             "config": {"workload": workload, "scene": f"scenes/{args.scene}.toml", "width": args.width,
                        "height": args.height, "spp": args.spp, "traced_spp": 4 * (args.spp // 4),
                        "mode": mode, "mis": args.mis,
-                       "parallelism": f"{'interleaved rows' if args.partition == 'interleave' else 'row stripes'} x{world}",
+                       "parallelism": f"{'interleaved rows' if args.partition == 'interleave' else 'row stripes'} x{world}"
+                                      ", host gather (gloo)" if world > 1 else "1 GPU",
                        "frame_sha1": digest,
                        "vertices_per_sample": round(total_vertices / n_samples, 4)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": kernel,
-                         "kernel_ms": round(dev_ms, 3),
-                         "alg_bytes_per_launch": alg_bytes,
-                         "model": "SURVEY 8(d): 88 B/sample + 280 B/vertex (canonical f32 SoA wavefront state)"},
+            "roofline": {"bound": "hbm",
+                         "achieved": round(achieved, 3) if achieved is not None else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 6) if achieved is not None else None,
+                         "traffic": traffic,
+                         "traffic_source": "profiles/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE per launch, "
+                                           "rocprofv3 passes over this command)" if traffic else None,
+                         "kernel": kernel, "kernel_ms": round(dev_ms, 3),
+                         "algorithmic_bytes_per_launch": alg_bytes,
+                         "wavefront_equiv_frac": round(model_bytes / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "wavefront_equiv_model": "SURVEY 8(d): 88 B/sample + 280 B/vertex (f32 SoA wavefront state), "
+                                                  "a model of what a wavefront would stream, not measured traffic"},
         }
-        # The megakernel's own bound is VALU issue: PMC instructions per vertex x the
-        # vertex rate of this run, against 1024 SIMDs x one wave-instruction per 4 cycles at 2.4 GHz
-        valu = load_valu(f"{args.scene} {mode}") if mode.startswith("megakernel") else None
-        if valu:
-            rate = valu["valu_inst_per_vertex"] * st["vertices"] / (dev_ms / 1e3)
-            peak = 1024 * 2.4e9 / 4
-            out["roofline"]["valu"] = {"achieved": round(rate / 1e9, 2), "peak": round(peak / 1e9, 2),
-                                       "unit": "G wave-instr/s", "frac": round(rate / peak, 4),
-                                       "inst_per_vertex": valu["valu_inst_per_vertex"], "source": valu["source"]}
+        mix = load_profile("pmc_valu.json", f"{args.scene} {mode}{' mis' if args.mis else ''}")
+        if mix and args.mode == "megakernel":
+            out["roofline"]["compute"] = compute_block(mix, st["vertices"], dev_ms)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

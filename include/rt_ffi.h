@@ -10,6 +10,8 @@
  *   rt_render           <- RenderJob::run's per-pixel loop   src/server.rs:157-199 calling
  *                          sample_pixel + gamma_correct      src/server.rs:320-368 (and the `as u8` at :187-189)
  *   rt_render_device    <- same, device-resident output, enqueued on a caller HIP stream (no host sync)
+ *   rt_render_multi     <- same, bands handed out dynamically to several devices (the row-band fan-out of
+ *                          RenderJob::run, server.rs:165-168), host gather
  *   rt_trace_rays       <- Scene::trace_ray                  src/scene.rs:272-289 (batch form, for parity tests)
  *
  * Conventions (mirroring the reference's):
@@ -21,8 +23,10 @@
  *     sample_pixel(x, height - row - 1, ...) (server.rs:179-186);
  *   - spp follows the reference: 4 * floor(spp / 4) samples are traced (server.rs:332); spp < 4
  *     renders black exactly like the reference.
- *   - randomness: counter-based (Philox4x32-10 -> xoroshiro128++), keyed by (seed, global pixel,
- *     subpixel, sample, depth); output is independent of tiling, device count and kernel mode.
+ *   - randomness: counter-based, one stream per camera sample: Philox4x32-10 keyed by the seed, with
+ *     counter (global pixel, sample, 0, subpixel), seeds an xoroshiro128++ stream that the path consumes
+ *     in the reference's draw order; output is independent of tiling, device count and
+ *     kernel mode.
  */
 #ifndef RT_FFI_H
 #define RT_FFI_H
@@ -33,7 +37,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2  /* 2: rt_render_params.row_step */
+#define RT_ABI_VERSION 3  /* 2: rt_render_params.row_step; 3: rt_render_multi */
 
 /* return codes */
 #define RT_OK 0
@@ -138,6 +142,21 @@ int rt_render(const rt_scene* scene, const rt_render_params* params, uint8_t* rg
  * Synchronous with respect to the stream only when stats != NULL. */
 int rt_render_device(const rt_scene* scene, const rt_render_params* params, void* d_rgb, void* d_sub,
                      void* stream, rt_render_stats* stats);
+
+/* One process, several devices (replaces the row-band fan-out of RenderJob::run,
+ * server.rs:165-168): the tile's rows are cut into bands of `band_rows` tile rows (<= 0: about 8 bands per
+ * worker) handed out dynamically from a host atomic counter to one worker thread per entry of `devices`
+ * (an ordinal may repeat: several workers on one device). A worker renders each band with the device path on
+ * its own streams (two bands in flight, so one band's tail overlaps the next band's start) and copies the RGB8
+ * rows straight into rgb_out: the gather is host-side, no collective. The image is byte-identical to rt_render
+ * of the same params (the RNG is keyed by global pixel). cancel is checked between bands. stats (optional):
+ * samples and vertices summed over the bands, device_ms = wall time of the whole call. */
+int rt_render_multi(const rt_scene* scene, const rt_render_params* params, const int32_t* devices, int32_t n_devices,
+                    int32_t band_rows, uint8_t* rgb_out, const volatile int32_t* cancel, rt_render_stats* stats);
+/* The band plan rt_render_multi hands out (no GPU): band b = tile rows [first_row[b], first_row[b] + rows[b]),
+ * in handout order. Returns the band count; writes at most `cap` entries (either array may be NULL). */
+int32_t rt_band_plan(int32_t tile_h, int32_t n_workers, int32_t band_rows, int32_t cap, int32_t* first_row,
+                     int32_t* rows);
 
 /* Scene::trace_ray on the device for n host rays: t, object id (-1: no hit), hit pos/normal. */
 int rt_trace_rays(const rt_scene* scene, int32_t device, int64_t n, const double* origins, const double* dirs,

@@ -704,12 +704,18 @@ static Mesh mesh_prism(V3 p, double w, double h, double d) {  // :839
                             4, 5, 7, 4, 6, 7, 2, 3, 7, 2, 6, 7, 0, 1, 5, 0, 4, 5};
     return mesh_new(v, idx);
 }
+// Rust's `usize::from_str` (geometry.rs:698-701 parse_face): one optional leading '+', then at
+// least one ASCII digit and nothing else; a value above usize::MAX is an error (PosOverflow).
 static bool parse_u64(const std::string& s, uint64_t* out) {
-    if (s.empty()) return false;
+    size_t i = (!s.empty() && s[0] == '+') ? 1 : 0;
+    if (i == s.size()) return false;
     uint64_t v = 0;
-    for (char ch : s) {
+    for (; i < s.size(); ++i) {
+        const char ch = s[i];
         if (ch < '0' || ch > '9') return false;
-        v = v * 10 + (uint64_t)(ch - '0');
+        const uint64_t d = (uint64_t)(ch - '0');
+        if (v > (UINT64_MAX - d) / 10) return false;
+        v = v * 10 + d;
     }
     *out = v;
     return true;

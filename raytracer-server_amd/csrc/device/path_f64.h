@@ -318,8 +318,9 @@ RT_DEV bool box_hit(const double* bx, const Ray& r, const RayInv& inv) {
 // which case no box contained in it can pass box_hit (its face points would be within rounding,
 // ~1e-11, of the ray). Exactness argument in DESIGN.md §Octree.
 // tmax: the caller's bound on a useful hit (closest analytic hit so far, or the shadow distance);
-// every mesh hit point lies in the mesh's bbox (the octree root box encloses all its triangles), so
-// a box entered only beyond tmax (with margin) cannot produce a hit that would be used.
+// every mesh hit point lies in DevMesh::cull_box (the root box united with the vertex bounds, so it
+// encloses every triangle even after the `scale` bbox quirk), so a box entered only beyond tmax
+// (with margin) cannot produce a hit that would be used.
 RT_DEV bool near_box(const double* bx, const Ray& r, const RayInv& inv, double pad, double tmax) {
     double t0 = 0.0, t1 = INFINITY;
     const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
@@ -498,7 +499,7 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
                        OctWalk& w) {
     if (m.n_nodes == 0) return false;
     RT_DBG(0);
-    if (!near_box(m.root_box, ray, inv, m.cull_pad, tmax)) return false;
+    if (!near_box(m.cull_box, ray, inv, m.cull_pad, tmax)) return false;
     RT_DBG(1);
     w.best = -1;
     w.bt = 0.0;
@@ -971,7 +972,7 @@ RT_DEV bool mesh_candidate(const DevScene& sc, const Ray& ray, const RayInv& inv
         const DevObject& o = sc.objects[T->gen_idx[i]];
         if (o.geom == GEOM_MESH && sc.meshes[o.mesh].n_nodes > 0) {
             const DevMesh& m = sc.meshes[o.mesh];
-            any |= near_box(m.root_box, ray, inv, m.cull_pad, tmax);
+            any |= near_box(m.cull_box, ray, inv, m.cull_pad, tmax);
         }
     }
     return any;

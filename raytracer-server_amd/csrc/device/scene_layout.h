@@ -40,7 +40,11 @@ struct alignas(16) DevObject {
 struct alignas(16) DevMesh {
     int32_t node_base, n_nodes, root_leaf, max_depth;  // root_leaf: leaf id when the root is a leaf, else -1
     int32_t tri_base, n_tris, bvh_base, bvh_n;  // bvh: this mesh's nodes in DevScene::bvh
-    double root_box[6];       // Octree.bounding_box (min xyz, max xyz)
+    double root_box[6];       // Octree.bounding_box (min xyz, max xyz): octant arithmetic of the walk
+    double cull_box[6];       // root_box united with the vertex bounds: the early-out culls (near_box).
+                              // The `scale` transform grows the stored box wrongly (geometry.rs:503-506),
+                              // so root_box alone need not enclose the triangles a leaf root or the
+                              // nearest-triangle loop tests without any box test (geometry.rs:886-903, 1276)
     double oct_center[8][3];  // centres of the ROOT box's octants: traversal order key (geometry.rs:1249-1260)
     double surface_area;      // Mesh.surface_area (mesh-light pdf, geometry.rs:591)
     double total_weight;      // sum of triangle areas (WeightedIndex total)

@@ -307,7 +307,8 @@ int parse_object(const Value& spec, const std::string& assets_dir, Scene* sc, st
     return RT_OK;
 }
 
-// Rust `str::parse::<usize>`: optional '+', then at least one ASCII digit, nothing else.
+// Rust `str::parse::<usize>`: optional '+', then at least one ASCII digit, nothing else; values
+// above usize::MAX (64-bit) are an error.
 bool parse_usize(const char* s, size_t n, uint64_t* out) {
     size_t i = 0;
     if (n && s[0] == '+') i = 1;
@@ -315,7 +316,9 @@ bool parse_usize(const char* s, size_t n, uint64_t* out) {
     uint64_t v = 0;
     for (; i < n; ++i) {
         if (s[i] < '0' || s[i] > '9') return false;
-        v = v * 10 + (uint64_t)(s[i] - '0');
+        const uint64_t d = (uint64_t)(s[i] - '0');
+        if (v > (UINT64_MAX - d) / 10) return false;
+        v = v * 10 + d;
     }
     *out = v;
     return true;

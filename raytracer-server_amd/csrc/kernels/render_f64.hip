@@ -332,7 +332,7 @@ RT_DEV bool next_mesh_walk_bvh(const DevScene& sc, const Ray& r, const RayInv& i
         const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
         if (o.geom != GEOM_MESH) continue;
         const DevMesh& m = sc.meshes[o.mesh];
-        if (m.bvh_n > 0 && near_box(m.root_box, r, inv, m.cull_pad, tmax)) {
+        if (m.bvh_n > 0 && near_box(m.cull_box, r, inv, m.cull_pad, tmax)) {
             mi = o.mesh;
             bvh_begin(m, tmax, w);
             return true;

@@ -52,6 +52,12 @@ struct Workspace {
     size_t tail_cap = 0;
     uint32_t* host_ctrl = nullptr;  // pinned mirror of ctrl
     hipEvent_t ev = nullptr;
+    // Pool bookkeeping (rt_api.cpp: take_workspace / give_workspace): `busy` is recorded on the
+    // render's stream after its last launch; the workspace is handed to another render only once
+    // that event has completed, or to a render on the same stream (ordered after it anyway).
+    hipEvent_t busy = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool in_flight = false;
 
     hipError_t ensure_counters();
     hipError_t ensure_slots(size_t n);

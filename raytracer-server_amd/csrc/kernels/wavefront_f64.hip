@@ -532,6 +532,7 @@ Workspace::~Workspace() {
     if (tail_buf) (void)hipFree(tail_buf);
     if (host_ctrl) (void)hipHostFree(host_ctrl);
     if (ev) (void)hipEventDestroy(ev);
+    if (busy) (void)hipEventDestroy(busy);
 }
 
 int wavefront_render_f64(const DevScene& sc, const RenderArgs& a_in, Workspace& ws, hipStream_t st,

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -9,6 +10,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_ffi.h"
@@ -245,9 +247,17 @@ void pack_scene(rt_scene* s) {
             dm.oct_center[i][2] = (lo.z + hi.z) / 2.0;
         }
         dm.surface_area = m.surface_area;
+        std::memcpy(dm.cull_box, rbox, sizeof rbox);
+        for (const D3& v : m.vertices) {
+            const double xyz[3] = {v.x, v.y, v.z};
+            for (int k = 0; k < 3; ++k) {
+                dm.cull_box[k] = std::fmin(dm.cull_box[k], xyz[k]);
+                dm.cull_box[3 + k] = std::fmax(dm.cull_box[3 + k], xyz[k]);
+            }
+        }
         {
             double mx = 1.0;
-            for (double v : rbox) mx = std::fmax(mx, std::fabs(v));
+            for (double v : dm.cull_box) mx = std::fmax(mx, std::fabs(v));
             dm.cull_pad = 1e-7 * mx;
         }
         double cum = 0.0;
@@ -548,20 +558,44 @@ int check_params(const rt_render_params* p) {
     return RT_OK;
 }
 
-std::unique_ptr<rt::Workspace> take_workspace(rt_scene* s, int device) {
+// Per-render scratch (ticket counter, subpixel buffer, split-tail buffer, wavefront streams) comes
+// from a per-scene pool. rt_render_device returns before its kernels finish, so a pooled workspace
+// may still be in use on its stream: it is reused only by a render on the same stream (stream order
+// serialises the two) or once the event recorded after its last launch has completed; otherwise a
+// new workspace is made (concurrent renders on one scene each get their own, rt_ffi.h).
+std::unique_ptr<rt::Workspace> take_workspace(rt_scene* s, int device, hipStream_t st) {
     std::lock_guard<std::mutex> lk(s->mu);
+    size_t pick = s->pool.size();
     for (size_t i = 0; i < s->pool.size(); ++i) {
-        if (s->pool[i]->device == device) {
-            std::unique_ptr<rt::Workspace> w = std::move(s->pool[i]);
-            s->pool.erase(s->pool.begin() + i);
-            return w;
+        rt::Workspace& w = *s->pool[i];
+        if (w.device != device) continue;
+        if (w.in_flight && w.last_stream == st) { pick = i; break; }  // stream-ordered after its last use
+        if (!w.in_flight || hipEventQuery(w.busy) == hipSuccess) {
+            if (pick == s->pool.size()) pick = i;
         }
+    }
+    (void)hipGetLastError();  // hipErrorNotReady from the queries is not an error
+    if (pick < s->pool.size()) {
+        std::unique_ptr<rt::Workspace> w = std::move(s->pool[pick]);
+        s->pool.erase(s->pool.begin() + pick);
+        return w;
     }
     auto w = std::make_unique<rt::Workspace>();
     w->device = device;
     return w;
 }
-void give_workspace(rt_scene* s, std::unique_ptr<rt::Workspace> w) {
+void give_workspace(rt_scene* s, std::unique_ptr<rt::Workspace> w, hipStream_t st) {
+    hipError_t e = hipSuccess;
+    if (!w->busy) e = hipEventCreateWithFlags(&w->busy, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(w->busy, st);
+    if (e != hipSuccess) {  // cannot track its completion: wait for it here
+        (void)hipGetLastError();
+        (void)hipStreamSynchronize(st);
+        w->in_flight = false;
+    } else {
+        w->in_flight = true;
+        w->last_stream = st;
+    }
     std::lock_guard<std::mutex> lk(s->mu);
     s->pool.push_back(std::move(w));
 }
@@ -608,7 +642,7 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
     }
     if (!fp32 && (p->flags & RT_FLAG_MESH_NEAREST) && !(p->flags & RT_FLAG_MEGAKERNEL))
         return fail(RT_E_INVAL, "RT_FLAG_MESH_NEAREST needs RT_FLAG_MEGAKERNEL");
-    std::unique_ptr<rt::Workspace> ws = take_workspace(s, p->device);
+    std::unique_ptr<rt::Workspace> ws = take_workspace(s, p->device, st);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (stats) {
         std::memset(stats, 0, sizeof *stats);
@@ -686,7 +720,7 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
     }
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
-    give_workspace(s, std::move(ws));
+    give_workspace(s, std::move(ws), st);
     if (out < 0) return fail(out, err);
     return out;
 }
@@ -837,6 +871,116 @@ int rt_render(const rt_scene* scene, const rt_render_params* p, uint8_t* rgb_out
     (void)hipStreamDestroy(st);
     if (rc < 0) return fail(rc, err);
     return rc;
+}
+
+int32_t rt_band_plan(int32_t tile_h, int32_t n_workers, int32_t band_rows, int32_t cap, int32_t* first_row,
+                     int32_t* rows) {
+    if (tile_h <= 0) return 0;
+    if (n_workers < 1) n_workers = 1;
+    int32_t b = band_rows;
+    if (b <= 0) b = std::max<int32_t>(1, (int32_t)(((int64_t)tile_h + 8LL * n_workers - 1) / (8LL * n_workers)));
+    const int32_t n = (int32_t)(((int64_t)tile_h + b - 1) / b);
+    for (int32_t i = 0; i < n && i < cap; ++i) {
+        if (first_row) first_row[i] = i * b;
+        if (rows) rows[i] = std::min(b, tile_h - i * b);
+    }
+    return n;
+}
+
+int rt_render_multi(const rt_scene* scene, const rt_render_params* p, const int32_t* devices, int32_t n_devices,
+                    int32_t band_rows, uint8_t* rgb_out, const volatile int32_t* cancel, rt_render_stats* stats) {
+    if (!scene || !rgb_out || !devices || n_devices <= 0) return fail(RT_E_INVAL, "null argument");
+    int rc = check_params(p);
+    if (rc != RT_OK) return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RT_E_NODEVICE, "no HIP device");
+    for (int32_t i = 0; i < n_devices; ++i)
+        if (devices[i] < 0 || devices[i] >= ndev) return fail(RT_E_INVAL, "device ordinal out of range");
+    const int32_t tw = p->tile_w, th = p->tile_h;
+    if ((size_t)tw * th == 0) return RT_OK;
+    const int32_t nb = rt_band_plan(th, n_devices, band_rows, 0, nullptr, nullptr);
+    std::vector<int32_t> first(nb), rows(nb);
+    rt_band_plan(th, n_devices, band_rows, nb, first.data(), rows.data());
+    int32_t bmax = 0;
+    for (int32_t r : rows) bmax = std::max(bmax, r);
+    const int64_t step = p->row_step > 1 ? p->row_step : 1;
+    std::atomic<int32_t> next{0};
+    std::atomic<int> err_code{RT_OK};
+    std::atomic<bool> stop{false};
+    std::atomic<int64_t> samples{0}, vertices{0};
+    std::atomic<int32_t> done{0};
+    std::mutex err_mu;
+    std::string err_msg;
+    const auto t0 = std::chrono::steady_clock::now();
+    rt_scene* s = const_cast<rt_scene*>(scene);
+
+    auto worker = [&](int32_t dev) {
+        auto record = [&](int code, const std::string& m) {
+            std::lock_guard<std::mutex> lk(err_mu);
+            if (err_code.load() == RT_OK) { err_code = code; err_msg = m; }
+            stop = true;
+        };
+        if (hipSetDevice(dev) != hipSuccess) { record(RT_E_HIP, "hipSetDevice"); return; }
+        constexpr int kSlots = 2;  // bands in flight per worker
+        hipStream_t st[kSlots] = {nullptr, nullptr};
+        uint8_t* d_rgb[kSlots] = {nullptr, nullptr};
+        uint8_t* h_rgb[kSlots] = {nullptr, nullptr};
+        int32_t pending[kSlots] = {-1, -1};
+        const size_t band_bytes = (size_t)bmax * tw * 3;
+        bool ok = true;
+        for (int k = 0; k < kSlots && ok; ++k) {
+            ok = hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) == hipSuccess &&
+                 hipMalloc(&d_rgb[k], band_bytes) == hipSuccess &&
+                 hipHostMalloc((void**)&h_rgb[k], band_bytes, hipHostMallocDefault) == hipSuccess;
+        }
+        if (!ok) record(RT_E_OOM, "rt_render_multi: band buffers");
+        // finishes band slot k: wait for its copy, put its rows into the caller's frame
+        auto drain = [&](int k) {
+            if (pending[k] < 0) return;
+            const int32_t b = pending[k];
+            pending[k] = -1;
+            if (hipStreamSynchronize(st[k]) != hipSuccess) { record(RT_E_HIP, "rt_render_multi: band sync"); return; }
+            std::memcpy(rgb_out + (size_t)first[b] * tw * 3, h_rgb[k], (size_t)rows[b] * tw * 3);
+            ++done;
+        };
+        for (int slot = 0; ok && !stop.load(); slot ^= 1) {
+            drain(slot);
+            if (stop.load() || (cancel && *cancel)) break;
+            const int32_t b = next.fetch_add(1);
+            if (b >= nb) break;
+            rt_render_params q = *p;
+            q.device = dev;
+            q.y0 = (int32_t)(p->y0 + (int64_t)first[b] * step);
+            q.tile_h = rows[b];
+            rt_render_stats bs;
+            const int r = render_enqueue(s, &q, d_rgb[slot], nullptr, st[slot], nullptr, stats ? &bs : nullptr);
+            if (r < 0) { record(r, g_err); break; }
+            if (stats) { samples += bs.samples; vertices += bs.vertices; }
+            if (hipMemcpyAsync(h_rgb[slot], d_rgb[slot], (size_t)rows[b] * tw * 3, hipMemcpyDeviceToHost, st[slot]) !=
+                hipSuccess) { record(RT_E_HIP, "rt_render_multi: band copy"); break; }
+            pending[slot] = b;
+        }
+        for (int k = 0; k < kSlots; ++k) drain(k);
+        for (int k = 0; k < kSlots; ++k) {
+            if (st[k]) (void)hipStreamSynchronize(st[k]);
+            if (d_rgb[k]) (void)hipFree(d_rgb[k]);
+            if (h_rgb[k]) (void)hipHostFree(h_rgb[k]);
+            if (st[k]) (void)hipStreamDestroy(st[k]);
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int32_t i = 0; i < n_devices; ++i) pool.emplace_back(worker, devices[i]);
+    for (auto& t : pool) t.join();
+    if (err_code.load() != RT_OK) return fail(err_code.load(), err_msg);
+    if (stats) {
+        std::memset(stats, 0, sizeof *stats);
+        stats->samples = samples.load();
+        stats->vertices = vertices.load();
+        stats->device_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        stats->kernel_launches[0] = nb;
+    }
+    if (done.load() < nb) return RT_CANCELLED;  // only a cancel leaves bands unrendered without an error
+    return RT_OK;
 }
 
 int rt_trace_rays(const rt_scene* scene, int32_t device, int64_t n, const double* origins, const double* dirs, double* t,

@@ -70,7 +70,7 @@ class SceneDesc(ctypes.Structure):
 
 
 _EXPORTS = ["rt_scene_load_toml", "rt_scene_create", "rt_scene_destroy", "rt_scene_info", "rt_scene_mesh",
-            "rt_render", "rt_render_device", "rt_trace_rays", "rt_trace_rays_flags", "rt_last_error", "rt_abi_version",
+            "rt_render", "rt_render_device", "rt_render_multi", "rt_band_plan", "rt_trace_rays", "rt_trace_rays_flags", "rt_last_error", "rt_abi_version",
             "rt_device_count"]
 
 
@@ -91,6 +91,11 @@ def _load():
     L.rt_render.argtypes = [vp, P(RenderParams), P(ctypes.c_uint8), P(ctypes.c_double), P(ctypes.c_int32),
                             P(RenderStats)]
     L.rt_render_device.argtypes = [vp, P(RenderParams), vp, vp, vp, P(RenderStats)]
+    L.rt_render_multi.argtypes = [vp, P(RenderParams), P(ctypes.c_int32), ctypes.c_int32, ctypes.c_int32,
+                                  P(ctypes.c_uint8), P(ctypes.c_int32), P(RenderStats)]
+    L.rt_band_plan.restype = ctypes.c_int32
+    L.rt_band_plan.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P(ctypes.c_int32),
+                               P(ctypes.c_int32)]
     L.rt_trace_rays.argtypes = [vp, ctypes.c_int32, ctypes.c_int64, P(ctypes.c_double), P(ctypes.c_double),
                                 P(ctypes.c_double), P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_double)]
     L.rt_trace_rays_flags.argtypes = [vp, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int64, P(ctypes.c_double),
@@ -271,6 +276,33 @@ def render_device(scene, params, d_rgb, d_sub=None, stream=None, stats=False):
                                 ctypes.c_void_p(stream) if stream else None,
                                 ctypes.byref(st) if st is not None else None))
     return st.as_dict() if st is not None else None
+
+
+def render_multi(scene, width, height, spp, devices, seed=0x5EED, tile=None, mis=False, band_rows=0, cancel=None,
+                 row_step=1, fp32=False, mesh_nearest=False):
+    """rt_render_multi: one worker thread per entry of `devices` (ordinals may repeat), bands of rows
+    handed out dynamically, RGB8 gathered on the host. Returns (rgb[th, tw, 3] u8, stats)."""
+    flags = FLAG_MEGAKERNEL | (FLAG_MIS if mis else 0) | (FLAG_FP32 if fp32 else 0) | \
+        (FLAG_MESH_NEAREST if mesh_nearest else 0)
+    p = make_params(width, height, spp, seed, tile, flags, devices[0], row_step)
+    rgb = np.zeros((p.tile_h, p.tile_w, 3), dtype=np.uint8)
+    devs = (ctypes.c_int32 * len(devices))(*devices)
+    st = RenderStats()
+    rc = _check(lib.rt_render_multi(scene.handle, ctypes.byref(p), devs, len(devices), band_rows,
+                                    _ptr(rgb, ctypes.c_uint8), ctypes.byref(cancel) if cancel is not None else None,
+                                    ctypes.byref(st)))
+    out = st.as_dict()
+    out["cancelled"] = rc == RT_CANCELLED
+    return rgb, out
+
+
+def band_plan(tile_h, n_workers, band_rows=0):
+    """The band plan rt_render_multi hands out: (first tile row, rows) per band, in handout order."""
+    n = lib.rt_band_plan(tile_h, n_workers, band_rows, 0, None, None)
+    first = np.zeros(max(1, n), dtype=np.int32)
+    rows = np.zeros(max(1, n), dtype=np.int32)
+    lib.rt_band_plan(tile_h, n_workers, band_rows, n, _ptr(first, ctypes.c_int32), _ptr(rows, ctypes.c_int32))
+    return first[:n].tolist(), rows[:n].tolist()
 
 
 def sample_pixel(x, y, width, height, samples_per_pixel, scene, seed=0x5EED, mis=False):

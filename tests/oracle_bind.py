@@ -13,7 +13,7 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
-LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
+LIB_PATH = os.environ.get("RT_ORACLE_LIB") or os.path.join(ORACLE_DIR, "liboracle.so")
 
 _lib = None
 
@@ -31,9 +31,8 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(
-            os.path.join(ORACLE_DIR, "oracle.cpp")
-        ):
+        if "RT_ORACLE_LIB" not in os.environ and (not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) <
+                                                  os.path.getmtime(os.path.join(ORACLE_DIR, "oracle.cpp"))):
             build()
         L = ctypes.CDLL(LIB_PATH)
         L.orc_scene_new.restype = ctypes.c_void_p

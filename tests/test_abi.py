@@ -20,7 +20,7 @@ def test_exports_every_declared_symbol(rt):
     assert len(names) >= 11
     for n in names:
         assert hasattr(rt.lib, n), f"missing export {n}"
-    assert rt.lib.rt_abi_version() == 2
+    assert rt.lib.rt_abi_version() == 3
 
 
 def test_exports_diagnostics(rt):
@@ -51,3 +51,21 @@ def test_errors_are_codes_not_crashes(rt):
     assert rt.lib.rt_scene_load_toml(b"/nonexistent.toml", None, ctypes.byref(h)) == -4
     assert b"nonexistent" in rt.lib.rt_last_error()
     assert rt.lib.rt_render(None, None, None, None, None, None) == -1
+
+
+def test_band_plan_covers_tile_in_order(rt):
+    """rt_render_multi's band plan (handed out in this order from a host atomic counter): the bands
+    partition the tile's rows [0, tile_h) contiguously, in increasing order, each non-empty; about 8
+    bands per worker by default."""
+    for th in (1, 7, 37, 450, 1080, 4096):
+        for workers in (1, 2, 3, 8):
+            for band in (0, 1, 5, 64, 5000):
+                first, rows = rt.band_plan(th, workers, band)
+                assert first[0] == 0 and all(r > 0 for r in rows)
+                assert all(first[i] + rows[i] == first[i + 1] for i in range(len(rows) - 1))
+                assert first[-1] + rows[-1] == th
+                if band > 0:
+                    assert all(r == min(band, th) for r in rows[:-1])
+                else:
+                    assert len(rows) <= 8 * workers and (th < 8 * workers or len(rows) >= 4 * workers)
+    assert rt.band_plan(0, 4, 0) == ([], [])

@@ -343,3 +343,123 @@ def test_extra_assets_parity(asset, rt, oracle, tmp_path):
     rgb_f, sub_f, _ = rt.render(sc, w, h, spp, SEED, want_sub=True, fp32=True)
     rgb_d, sub_d, _ = rt.render(sc, w, h, spp, SEED, want_sub=True, megakernel=True, mesh_nearest=True)
     _assert_fp32_stats(sub_f, sub_d, rgb_f, rgb_d, f"{asset}/f32")
+
+
+# ---------------------------------------------------------------- reference quirks off the 3 scenes
+QUIRK_SCENE = """
+[camera]
+pos = [0.0, 6.0, 60.0]
+dir = [0.0, -0.1, -1.0]
+[[objects]]
+emitted = [12.0, 12.0, 12.0]
+brdf = { type = "diffuse", kd = [0.0, 0.0, 0.0] }
+geometry = { type = "cube", pos = [6.0, 14.0, -4.0], size = 4.0 }
+transforms = [ { rotate_y = 0.3 } ]
+[[objects]]
+brdf = { type = "phong", kd = 0.5, ks = 0.3, power = 8, color_d = [0.7, 0.6, 0.5], color_s = [1.0, 1.0, 1.0] }
+geometry = { type = "plane", pos = [0.0, -5.0, 0.0], n = [0.0, 1.0, 0.0] }
+[[objects]]
+brdf = { type = "diffuse", kd = [0.6, 0.6, 0.75] }
+geometry = { type = "plane", pos = [0.0, 0.0, -30.0], n = [0.0, 0.0, 1.0] }
+[[objects]]
+brdf = { type = "phong", kd = 0.2, ks = 0.7, power = 24, color_d = [0.9, 0.3, 0.3], color_s = [1.0, 1.0, 1.0] }
+geometry = { type = "sphere", pos = [-8.0, 0.0, 2.0], r = 5.0 }
+[[objects]]
+brdf = { type = "specular", ks = [0.95, 0.95, 0.95] }
+geometry = { type = "sphere", pos = [9.0, -1.0, 6.0], r = 4.0 }
+[[objects]]
+brdf = { type = "diffuse", kd = [0.8, 0.8, 0.8] }
+geometry = { type = "prism", pos = [-2.0, -5.0, -12.0], size = [6.0, 9.0, 5.0] }
+"""
+
+
+def test_phong_and_mesh_light_parity(rt, oracle, tmp_path):
+    """Phong BRDFs with the reference's unrotated lobes (scene.rs:56-98) and a
+    triangle-mesh emitter (the first emitting object is the light, scene.rs:129-137) sampled with
+    WeightedIndex + Triangle::sample's missing `+ a` (geometry.rs:588-592, 622-635), on the f64
+    megakernel and wavefront against the oracle at the 1e-9 / RGB8 bounds; MIS on and off."""
+    p = tmp_path / "quirks.toml"
+    p.write_text(QUIRK_SCENE)
+    sc, orc = rt.Scene.from_toml(str(p)), oracle.OracleScene(str(p))
+    assert sc.info()["light"] == 0 == orc.light and orc.objects[0] == "cube"
+    w, h, spp = 64, 48, 16
+    for mis in (False, True):
+        rgb_o, sub_o, st_o = orc.render(w, h, spp, SEED, mis=mis)
+        assert rgb_o.mean() > 5  # the frame is not black: light reaches the camera
+        for mk in (True, False):
+            rgb_g, sub_g, st = rt.render(sc, w, h, spp, SEED, megakernel=mk, mis=mis, want_sub=True)
+            assert 0.9 * st_o["vertices"] <= st["vertices"] <= st_o["vertices"]
+            _assert_parity(rgb_g, sub_g, rgb_o, sub_o, f"quirks/{'mk' if mk else 'wf'}/{'mis' if mis else 'nee'}")
+
+
+ROOT_LEAF_OBJ = """v 0 0 0
+v 4 0 0
+v 0 0 4
+v 0 5 0
+v 4 5 4
+f 1 2 3
+f 1 2 4
+f 1 3 4
+f 2 3 4
+f 2 5 4
+f 3 5 4
+"""
+ROOT_LEAF_SCENE = """
+[camera]
+pos = [50.0, 30.0, 160.0]
+dir = [0.0, -0.1, -1.0]
+[[objects]]
+brdf = { type = "diffuse", kd = [0.75, 0.75, 0.75] }
+geometry = { type = "plane", pos = [0.0, 0.0, 0.0], n = [0.0, 1.0, 0.0] }
+[[objects]]
+brdf = { type = "diffuse", kd = [0.75, 0.25, 0.25] }
+geometry = { type = "plane", pos = [0.0, 0.0, 0.0], n = [0.0, 0.0, 1.0] }
+[[objects]]
+brdf = { type = "diffuse", kd = [0.9, 0.9, 0.9] }
+geometry = { type = "mesh", path = "pyr.obj" }
+transforms = [ { scale = 6.0 }, { scale = -0.8 }, { translate = [50.0, 20.0, 60.0] } ]
+[[objects]]
+emitted = [50.0, 50.0, 50.0]
+brdf = { type = "diffuse", kd = [0.0, 0.0, 0.0] }
+geometry = { type = "sphere", pos = [50.0, 70.0, 100.0], r = 4.0 }
+"""
+
+
+def test_root_leaf_mesh_with_scale_quirk(rt, oracle, tmp_path):
+    """A mesh of <= 9 triangles is a single octree leaf, which the reference tests without any box
+    (geometry.rs:1237-1241, 1276-1293). A negative `scale` below -0.5 leaves the stored bounding box
+    smaller than the triangles (geometry.rs:503-506), so the device's early-out culls must use a box
+    that encloses both (DevMesh::cull_box): trace_ray bit-exact against the oracle, with hits outside
+    the stored box, in both mesh semantics, and a render at parity."""
+    (tmp_path / "assets").mkdir()
+    (tmp_path / "assets" / "pyr.obj").write_text(ROOT_LEAF_OBJ)
+    p = tmp_path / "leaf.toml"
+    p.write_text(ROOT_LEAF_SCENE)
+    sc, orc = rt.Scene.from_toml(str(p)), oracle.OracleScene(str(p))
+    info = sc.info()
+    assert info["nodes"] == 1 and info["leaves"] == 1
+    m = sc.mesh(2)
+    lo, hi = m["bbox"][:3], m["bbox"][3:]
+    v = m["vertices"]
+    assert np.any(v < lo - 1e-9) and np.any(v > hi + 1e-9)  # the stored box no longer encloses the mesh
+    rng = np.random.default_rng(77)
+    n = 20000
+    tgt = rng.uniform(v.min(0) - 1, v.max(0) + 1, size=(n, 3))
+    o = rng.uniform([5, 2, 80], [95, 60, 200], size=(n, 3))
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    t_g, id_g, p_g, n_g = sc.trace_ray(o, d)
+    t_o, id_o, p_o, n_o = orc.trace(o, d)
+    exact = (id_g == id_o) & (t_g == t_o) & np.all(p_g == p_o, axis=1) & np.all(n_g == n_o, axis=1)
+    assert exact.all(), f"{np.count_nonzero(~exact)} of {n} hits differ"
+    on_mesh = id_o == 2
+    outside = on_mesh & np.any((p_o < lo - 1e-6) | (p_o > hi + 1e-6), axis=1)
+    assert on_mesh.sum() > 1000 and outside.sum() > 100, (on_mesh.sum(), outside.sum())
+    orc_n = oracle.OracleScene(str(p), mesh_nearest=True)
+    t_g, id_g, p_g, n_g = sc.trace_ray(o, d, mesh_nearest=True)
+    t_o, id_o, p_o, n_o = orc_n.trace(o, d)
+    assert np.array_equal(id_g, id_o) and np.array_equal(t_g, t_o) and np.array_equal(p_g, p_o)
+    rgb_o, sub_o, _ = orc.render(64, 48, 16, SEED)
+    for mk in (True, False):
+        rgb_g, sub_g, _ = rt.render(sc, 64, 48, 16, SEED, megakernel=mk, want_sub=True)
+        _assert_parity(rgb_g, sub_g, rgb_o, sub_o, f"root-leaf/{'mk' if mk else 'wf'}")

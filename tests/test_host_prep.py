@@ -98,6 +98,36 @@ def test_obj_errors(rt, tmp_path):
     assert m["indices"].tolist() == [[0, 1, 2]]
 
 
+@pytest.mark.parametrize("face,ok", [
+    ("f 1/1/1 +2/2/2 3", True),        # usize::from_str accepts one leading '+'
+    ("f 1 2 +3", True),
+    ("f 1 2 +", False),                # '+' alone
+    ("f 1 2 ++3", False),
+    ("f 1 2 -3", False),               # no sign for usize
+    ("f 1 2 18446744073709551616", False),  # usize::MAX + 1: PosOverflow
+    ("f 1 2 3/", False),               # empty part after '/'
+    ("f 1 2 3x", False),
+])
+def test_obj_face_index_parse_product_and_oracle_agree(rt, oracle, tmp_path, face, ok):
+    """geometry.rs:698-701 parse_face (Rust `usize::from_str`): the product's OBJ reader and the
+    oracle's restatement must accept and reject the same face tokens."""
+    (tmp_path / "assets").mkdir()
+    base = GOOD + '\n[[objects]]\nbrdf = { type = "diffuse", kd = [1,1,1] }\ngeometry = { type = "mesh", path = "m.obj" }\n'
+    p = _write(tmp_path, base)
+    (tmp_path / "assets" / "m.obj").write_text(f"v 0 0 0\nv 1 0 0\nv 0 1 0\n{face}\n")
+    try:
+        s = rt.Scene.from_toml(p)
+        prod = s.mesh(2)["indices"].tolist() == [[0, 1, 2]]
+    except rt.RtError:
+        prod = False
+    try:
+        oracle.OracleScene(p)
+        orc = True
+    except RuntimeError:
+        orc = False
+    assert prod == ok and orc == ok
+
+
 def test_scene_create_from_desc_matches_toml(rt):
     """rt_scene_create (the host-keeps-its-loader boundary) builds the same octree as the TOML path."""
     t = rt.Scene.from_toml(scene_path("flying_unicorn"))

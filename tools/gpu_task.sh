@@ -1,0 +1,90 @@
+#!/bin/bash
+# One parametrised runner for every GPU-box job (run through gpurun from the repo root):
+#   bash tools/gpu_task.sh TASK [TASK ...]     tasks run in order; the first failure ends the call
+# Tasks:
+#   tests            python -m pytest tests -m gpu (log: gpurun_out/$TAG/pytest_gpu.log)
+#   tests:EXPR       the same with -k EXPR
+#   smoke            __graft_entry__.smoke()
+#   bench            python bench.py (headline line, cpu_baseline included)
+#   trace            rocprofv3 --kernel-trace --stats of `python bench.py --no-cpu-baseline`
+#   benchpmc         FETCH_SIZE / WRITE_SIZE passes over `bench.py --steps 1 --warmup 0` -> $OUT/pmc_traffic.json
+#   configs          tools/configs_bench.py (every BASELINE config, one GPU)
+#   pmc:SCENE:W:H:SPP[:mis]   counter passes on one megakernel render (tools/prof_render.py):
+#                    HBM traffic (FETCH_SIZE / WRITE_SIZE), L2 hit rate (TCC_HIT / TCC_MISS), clock
+#                    (GRBM_GUI_ACTIVE) and the SQ instruction mix, each pass a run of its own
+#   py:SCRIPT[:ARGS] python SCRIPT ARGS (":" separates args), e.g. py:tools/configs_bench.py:--quick
+# Env: TAG (output subdirectory, default "run"), BENCH_ARGS (extra bench.py arguments).
+export TMPDIR=/tmp
+TAG=${TAG:-run}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+
+fail() { echo "FAIL: $1"; [ -f "$2" ] && tail -30 "$2"; exit 1; }
+
+# SQ passes: at most 8 SQ counters each
+SQ1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU"
+SQ2="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64"
+SQ3="SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_LDS"
+
+pmc_pass() {  # name counters... -- command
+    local name=$1; shift
+    local ctr=()
+    while [ "$1" != "--" ]; do ctr+=("$1"); shift; done
+    shift
+    timeout -s KILL 120 rocprofv3 --pmc "${ctr[@]}" -d "$OUT/$name" -o run --output-format csv -- "$@" \
+        > "$OUT/$name.log" 2>&1 || fail "pmc pass $name" "$OUT/$name.log"
+}
+
+for task in "$@"; do
+    IFS=: read -r -a A <<< "$task"
+    case "${A[0]}" in
+    tests)
+        K=()
+        [ -n "${A[1]}" ] && K=(-k "${A[1]}")
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
+            > "$OUT/pytest_gpu.log" 2>&1 || fail tests "$OUT/pytest_gpu.log"
+        tail -1 "$OUT/pytest_gpu.log" ;;
+    smoke)
+        timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || fail smoke "$OUT/smoke.log"
+        tail -1 "$OUT/smoke.log" ;;
+    bench)
+        timeout -k 10 600 python bench.py $BENCH_ARGS > "$OUT/bench.log" 2>&1 || fail bench "$OUT/bench.log"
+        tail -1 "$OUT/bench.log" ;;
+    trace)
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
+            python bench.py --no-cpu-baseline $BENCH_ARGS > "$OUT/trace.log" 2>&1 || fail trace "$OUT/trace.log"
+        tail -1 "$OUT/trace.log" | cut -c1-300 ;;
+    benchpmc)
+        # HBM traffic of the bench's own timed launch (roofline.traffic): separate FETCH / WRITE passes
+        B=(python bench.py --steps 1 --warmup 0 --no-cpu-baseline $BENCH_ARGS)
+        pmc_pass bench_fetch FETCH_SIZE -- "${B[@]}"
+        pmc_pass bench_write WRITE_SIZE -- "${B[@]}"
+        key=$(tail -1 "$OUT/bench_fetch.log" | python -c "import json,sys;d=json.loads(sys.stdin.read());print(d['config']['workload'],d['config']['mode'])")
+        python tools/pmc_traffic.py "$OUT/bench_fetch/run_counter_collection.csv" "$OUT/bench_write/run_counter_collection.csv" \
+            "$key" --out "$OUT/pmc_traffic.json" || fail benchpmc ;;
+    configs)
+        timeout -k 10 900 python -u tools/configs_bench.py > "$OUT/configs.log" 2>&1 || fail configs "$OUT/configs.log"
+        cat "$OUT/configs.log" ;;
+    pmc)
+        scene=${A[1]}; w=${A[2]}; h=${A[3]}; spp=${A[4]}; extra=${A[5]}
+        P=(python tools/prof_render.py "$scene" "$w" "$h" "$spp" mk $extra)
+        key="${scene}_${w}x${h}x${spp}${extra:+_$extra}"
+        timeout -k 10 120 "${P[@]}" > "$OUT/${key}_plain.log" 2>&1 || fail "plain $key" "$OUT/${key}_plain.log"
+        cat "$OUT/${key}_plain.log"
+        pmc_pass "${key}_fetch" FETCH_SIZE GRBM_GUI_ACTIVE -- "${P[@]}"
+        pmc_pass "${key}_write" WRITE_SIZE -- "${P[@]}"
+        pmc_pass "${key}_tcc" TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE -- "${P[@]}"
+        pmc_pass "${key}_sq1" $SQ1 -- "${P[@]}"
+        pmc_pass "${key}_sq2" $SQ2 -- "${P[@]}"
+        pmc_pass "${key}_sq3" $SQ3 -- "${P[@]}"
+        echo "pmc $key ok" ;;
+    py)
+        script=${A[1]}
+        timeout -k 10 900 python -u "$script" "${A[@]:2}" > "$OUT/$(basename "$script" .py).log" 2>&1 \
+            || fail "$script" "$OUT/$(basename "$script" .py).log"
+        tail -40 "$OUT/$(basename "$script" .py).log" ;;
+    *)
+        fail "unknown task $task" ;;
+    esac
+done
+echo "gpu_task: all done ($*)"

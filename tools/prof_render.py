@@ -1,4 +1,10 @@
-"""One render through the C ABI for profiling runs: python tools/prof_render.py SCENE W H SPP [mk|wf|f32] [mis] [nearest]"""
+"""One render through the C ABI for profiling runs:
+python tools/prof_render.py SCENE W H SPP [mk|wf|f32] [mis] [nearest]
+
+A small warm-up render of the same scene runs first (module load, scene upload), so the last
+dispatch of the render kernel in a rocprofv3 pass is the measured render; the line printed at the
+end carries its device time and exact path-vertex count (tools/pmc_report.py reads both)."""
+import hashlib
 import os
 import sys
 import time
@@ -12,11 +18,13 @@ mode = sys.argv[5] if len(sys.argv) > 5 else "mk"
 mis = "mis" in sys.argv[6:]
 nearest = "nearest" in sys.argv[6:]  # RT_FLAG_MESH_NEAREST (BVH)
 s = rt_amd.Scene.from_toml(os.path.join(REPO, "scenes", f"{scene}.toml"))
+kw = dict(megakernel=(mode == "mk"), mis=mis, mesh_nearest=nearest, fp32=(mode == "f32"))
+rt_amd.render(s, 64, 48, 4, **kw)  # warm-up
 t = time.perf_counter()
-rgb, _, st = rt_amd.render(s, w, h, spp, megakernel=(mode == "mk"), mis=mis, mesh_nearest=nearest,
-                           fp32=(mode == "f32"))
+rgb, _, st = rt_amd.render(s, w, h, spp, **kw)
 dt = time.perf_counter() - t
 n = w * h * 4 * (spp // 4)
-print(f"{scene} {w}x{h}x{spp} {mode}{' mis' if mis else ''}{' nearest' if nearest else ''}: {dt*1e3:.1f} ms wall, {st['device_ms']:.1f} ms device, "
-      f"{n / st['device_ms'] / 1e3:.1f} Msamples/s, {st['vertices'] / max(1, n):.3f} vertices/sample, "
-      f"iterations {st['iterations']}, rgb sha1 {__import__('hashlib').sha1(rgb.tobytes()).hexdigest()[:12]}")
+print(f"{scene} {w}x{h}x{spp} {mode}{' mis' if mis else ''}{' nearest' if nearest else ''}: {dt*1e3:.1f} ms wall, "
+      f"{st['device_ms']:.1f} ms device, {n / st['device_ms'] / 1e3:.1f} Msamples/s, samples {n}, "
+      f"vertices {st['vertices']}, {st['vertices'] / max(1, n):.3f} vertices/sample, iterations {st['iterations']}, "
+      f"rgb sha1 {hashlib.sha1(rgb.tobytes()).hexdigest()[:12]}")
