@@ -421,35 +421,51 @@ RT_DEV uint32_t octant_mask(const double* mn, const double* mx, const Ray& r, co
     return m;
 }
 
-// Diagnostic build only (make EXTRA=-DRT_DEBUG_COUNTERS=1): traversal work counters.
+// Diagnostic builds only (make EXTRA="-DRT_DEBUG_COUNTERS=1 -DRT_DEBUG_TIMERS=1", tools/dbg_mesh.py).
+// Counters and timers accumulate per block in LDS (LDS atomics: global atomics from every lane on a
+// few addresses serialised the instrumented kernels and distorted what they measured) and are
+// flushed to the g_dbg* arrays once per block by the megakernels (RT_DBG_TINIT / RT_DBG_TFLUSH);
+// other kernels' counts are dropped.
 #if RT_DEBUG_COUNTERS
 // 0 walks, 1 past cull, 2 node visits, 3 leaves, 4 tri tests, 5 steps; mesh megakernel (per wave):
 // 8 iterations, 9 lanes in the vertex phase, 10 walk-loop steps, 11 walking lanes over those steps
 __device__ unsigned long long g_dbg[16];
-#define RT_DBG(i) atomicAdd(&g_dbg[i], 1ull)
-#define RT_DBG_WAVE(i, pred) do { const unsigned long long m_ = __ballot(pred); if (__lane_id() == 0) atomicAdd(&g_dbg[i], (unsigned long long)__popcll(m_)); } while (0)
+__shared__ unsigned long long s_dbg_cnt[16];
+#define RT_DBG(i) atomicAdd(&s_dbg_cnt[i], 1ull)
+#define RT_DBG_WAVE(i, pred) do { const unsigned long long m_ = __ballot(pred); if (__lane_id() == 0) atomicAdd(&s_dbg_cnt[i], (unsigned long long)__popcll(m_)); } while (0)
 // lane utilisation of code region i (< 16): [2i] wave entries, [2i+1] active lanes summed over them
 __device__ unsigned long long g_dbg_region[32];
-#define RT_DBG_REGION(i) do { const unsigned long long m_ = __ballot(1); if (__lane_id() == __ffsll((long long)m_) - 1) { atomicAdd(&g_dbg_region[2 * (i)], 1ull); atomicAdd(&g_dbg_region[2 * (i) + 1], (unsigned long long)__popcll(m_)); } } while (0)
+__shared__ unsigned long long s_dbg_reg[32];
+#define RT_DBG_REGION(i) do { const unsigned long long m_ = __ballot(1); if (__lane_id() == __ffsll((long long)m_) - 1) { atomicAdd(&s_dbg_reg[2 * (i)], 1ull); atomicAdd(&s_dbg_reg[2 * (i) + 1], (unsigned long long)__popcll(m_)); } } while (0)
+#define RT_DBG_CINIT() do { if (threadIdx.x < 16) s_dbg_cnt[threadIdx.x] = 0; if (threadIdx.x < 32) s_dbg_reg[threadIdx.x] = 0; } while (0)
+#define RT_DBG_CFLUSH() do { if (threadIdx.x < 16) atomicAdd(&g_dbg[threadIdx.x], s_dbg_cnt[threadIdx.x]); if (threadIdx.x < 32) atomicAdd(&g_dbg_region[threadIdx.x], s_dbg_reg[threadIdx.x]); } while (0)
 #else
 #define RT_DBG_REGION(i) ((void)0)
 #define RT_DBG(i) ((void)0)
 #define RT_DBG_WAVE(i, pred) ((void)0)
+#define RT_DBG_CINIT() ((void)0)
+#define RT_DBG_CFLUSH() ((void)0)
 #endif
-// Diagnostic build only (make EXTRA=-DRT_DEBUG_TIMERS=1): wave time per code region i (< 16) in
-// s_memtime ticks, summed per wave in LDS (no global atomics on the path) and flushed to
+// Wave time per code region i (< 16) in s_memtime ticks, summed per wave in LDS and flushed to
 // g_dbg_time at the kernel's end; blocks of 256 threads (4 waves).
 #if RT_DEBUG_TIMERS
 __device__ unsigned long long g_dbg_time[16];
 __shared__ unsigned long long s_dbg_time[4 * 16];
-#define RT_DBG_TINIT() do { if (threadIdx.x < 64) s_dbg_time[threadIdx.x] = 0; __syncthreads(); } while (0)
 #define RT_DBG_TSTART(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define RT_DBG_TEND(i, v) do { const uint64_t d_ = __builtin_amdgcn_s_memtime() - (v); const unsigned long long m_ = __ballot(1); if (__lane_id() == __ffsll((long long)m_) - 1) atomicAdd(&s_dbg_time[(threadIdx.x >> 6) * 16 + (i)], (unsigned long long)d_); } while (0)
-#define RT_DBG_TFLUSH() do { __syncthreads(); if (threadIdx.x < 64) atomicAdd(&g_dbg_time[threadIdx.x & 15], s_dbg_time[threadIdx.x]); } while (0)
+#define RT_DBG_TIMERS_INIT() do { if (threadIdx.x < 64) s_dbg_time[threadIdx.x] = 0; } while (0)
+#define RT_DBG_TIMERS_FLUSH() do { if (threadIdx.x < 64) atomicAdd(&g_dbg_time[threadIdx.x & 15], s_dbg_time[threadIdx.x]); } while (0)
 #else
-#define RT_DBG_TINIT() ((void)0)
 #define RT_DBG_TSTART(v) ((void)0)
 #define RT_DBG_TEND(i, v) ((void)0)
+#define RT_DBG_TIMERS_INIT() ((void)0)
+#define RT_DBG_TIMERS_FLUSH() ((void)0)
+#endif
+#if RT_DEBUG_COUNTERS || RT_DEBUG_TIMERS
+#define RT_DBG_TINIT() do { RT_DBG_CINIT(); RT_DBG_TIMERS_INIT(); __syncthreads(); } while (0)
+#define RT_DBG_TFLUSH() do { __syncthreads(); RT_DBG_CFLUSH(); RT_DBG_TIMERS_FLUSH(); } while (0)
+#else
+#define RT_DBG_TINIT() ((void)0)
 #define RT_DBG_TFLUSH() ((void)0)
 #endif
 

@@ -50,7 +50,14 @@ struct alignas(16) DevMesh {
     double total_weight;      // sum of triangle areas (WeightedIndex total)
     double cull_pad;          // near_box padding: 1e-7 * max(1, |box coordinates|)
     int32_t btri_base, pad0, pad1, pad2;  // first of this mesh's n_tris BVH-order triangles (DevScene::btris)
+    // Flat octree (the cubes): the root is a leaf, or a parent whose children are all leaves, with at
+    // most kFlatMaxTris triangles and every leaf list in triangle order. flat_leaf[j / 4] byte j % 4 =
+    // the leaves (octant bits; bit 0 for a root leaf) that hold triangle j; flat_kids = octants with a
+    // leaf. render_flat_f64.hip evaluates the reference's walk on these tables (flat_query).
+    int32_t flat, flat_kids, flat_root_leaf, pad3;
+    uint32_t flat_leaf[8];
 };
+constexpr int kFlatMaxTris = 32;
 
 // BVH over a mesh's triangles for the nearest-triangle mode (RT_FLAG_MESH_NEAREST), nodes in DFS
 // pre-order: an inner node's left child is the next node, `a` its right child, `axis` the split

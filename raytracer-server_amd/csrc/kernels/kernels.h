@@ -20,6 +20,9 @@ struct RenderArgs {
     // samples; a chunk's lane stores each sample's radiance in tail_buf[sub - n_whole][sample][3]
     // and k_tail_sum adds them up in sample order afterwards (the same sequential sum)
     int32_t n_whole, chunk_lg;
+    // whole subpixels are handed out in runs of unit_subs consecutive subpixels per ticket (n_wunits
+    // tickets): at low spp a ticket per subpixel makes the one global counter's atomics the bottleneck
+    int32_t unit_subs, n_wunits;
     uint64_t seed;
     double cx[3], cy[3];  // camera frame (server.rs:330-331), computed on the host
     double inv_n;         // 1.0 / n_samples (server.rs:358)
@@ -29,11 +32,16 @@ struct RenderArgs {
     const int32_t* cancel;         // optional device view of the host cancel flag (mapped memory)
     double* tail_buf;              // split-tail sample radiance (see n_whole)
     int32_t f32_brute;             // f32 mode: meshes of <= f32_brute triangles are tested without the BVH
+    int32_t all_flat;              // every mesh is a flat octree (DevMesh::flat) and there are <= 4 of them
 };
 
 // tail_buf / tail_cap: scratch for the split tail (bytes); the launcher sizes the tail to fit it.
 hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
                                  double* tail_buf, size_t tail_cap, hipStream_t st);
+// Block-synchronous kernel for flat-octree mesh scenes (render_flat_f64.hip); called by
+// launch_megakernel_f64 after the ticket counter is reset.
+hipError_t launch_megakernel_flat_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
+                                      double* tail_buf, size_t tail_cap, int refill, hipStream_t st);
 // f32 perf mode (render_f32.hip): writes the subpixel means to sub_buf like the f64 megakernel.
 hipError_t launch_megakernel_f32(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
                                  hipStream_t st);

@@ -1,0 +1,127 @@
+// Scheduling shared by the persistent megakernels (render_f64.hip, render_flat_f64.hip): wave-
+// aggregated tickets on one global counter, work units (runs of whole subpixels, split-tail chunks),
+// and the host-side planning of both.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+
+#include "kernels.h"
+
+namespace rt {
+
+// Wave-aggregated ticket: every lane with `want` gets the next value of *counter (one atomic per
+// wave). All 64 lanes must call it together.
+__device__ __forceinline__ long wave_ticket(uint32_t* counter, bool want) {
+    const unsigned long long m = __ballot(want);
+    if (m == 0ull) return -1;
+    const int lane = __lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+    return want ? (long)base + __popcll(below) : -1;
+}
+
+// Adds the wave's vertex counts to *counter and zeroes them. All 64 lanes must call it together.
+__device__ __forceinline__ void flush_count(unsigned long long* counter, uint32_t& n) {
+    if (!counter) return;
+    unsigned long long v = n;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (__lane_id() == 0 && v) atomicAdd(counter, v);
+    n = 0;
+}
+
+// Work unit of ticket t: the whole subpixels [id, end) (t < n_wunits: a run of unit_subs consecutive
+// subpixels, samples [0, n) each), or chunk c = t - n_wunits of the split tail (subpixel
+// n_whole + c / cps, samples [k 2^chunk_lg, (k + 1) 2^chunk_lg), k = c % cps; end = id + 1).
+__device__ __forceinline__ void unit_of(const RenderArgs& a, long t, int& id, int& end, int& s) {
+    if (t < a.n_wunits) {
+        id = (int)t * a.unit_subs;
+        end = min(id + a.unit_subs, a.n_whole);
+        s = 0;
+    } else {
+        const uint32_t c = (uint32_t)(t - a.n_wunits);  // < n_split * cps < 2^32 (plan_tail)
+        const uint32_t q = c / (uint32_t)a.tail_cps;
+        id = a.n_whole + (int)q;
+        end = id + 1;
+        s = (int)(c - q * (uint32_t)a.tail_cps) << a.chunk_lg;
+    }
+}
+// Is sample s2 (> s) part of the unit that holds sample s?
+__device__ __forceinline__ bool unit_has(const RenderArgs& a, int id, int s, int s2) {
+    return s2 < a.n_samples && (id < a.n_whole || (s2 >> a.chunk_lg) == (s >> a.chunk_lg));
+}
+// Is sample s + 1 still part of the unit that holds sample s? (No register for the unit's end: a
+// split unit ends at the next multiple of 2^chunk_lg.)
+__device__ __forceinline__ bool unit_has_next(const RenderArgs& a, int id, int s) {
+    return s + 1 < a.n_samples && (id < a.n_whole || ((s + 1) >> a.chunk_lg) == (s >> a.chunk_lg));
+}
+
+__device__ __forceinline__ bool lane_id_is0() { return __lane_id() == 0; }
+
+// Resident grid of a persistent kernel: as many 256-thread blocks as fit on the device at once.
+template <class K>
+static inline long resident_blocks(K kernel, long want) {
+    int dev = 0, ncu = 256, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    return std::max(1L, std::min((long)ncu * per_cu, want));
+}
+
+static inline int env_int(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    return v ? std::atoi(v) : dflt;
+}
+
+#ifndef RT_MK_W4
+#define RT_MK_W4 4  // waves/SIMD of the analytic-scene kernel (A/B builds: -DRT_MK_W4=5)
+#endif
+// Split tail (RenderArgs::n_whole): the last subpixels are handed out in chunks of samples, so the
+// frame does not end with lanes idling while others finish a whole subpixel (the 1/N-sized frames
+// of an N-GPU run hold only a few subpixels per lane). Up to one subpixel per resident lane is
+// split, limited by the scratch buffer (tail_cap bytes); RT_MK_TAIL=0 disables it.
+// Runs of whole subpixels per ticket: about RT_MK_UNIT_SAMPLES (256) samples per ticket, but at least
+// RT_MK_UNITS_PER_LANE (16) runs per resident lane, so the frame's end stays balanced (2 runs per lane
+// left the unicorn's lanes idling behind a few long runs: -30%). At 1024 spp that is one subpixel per
+// ticket; at 64 spp (16 samples per subpixel) a ticket per subpixel put every wave behind the one
+// counter's atomic every few iterations (1920x1080x64: 2.3x the 1024-spp time per sample).
+static inline void plan_units(RenderArgs& a, long lanes) {
+    static const int target = std::max(1, env_int("RT_MK_UNIT_SAMPLES", 256));
+    static const int per_lane = std::max(1, env_int("RT_MK_UNITS_PER_LANE", 16));
+    long b = std::max(1, target / std::max(1, a.n_samples));
+    b = std::max(1L, std::min(b, (long)a.n_whole / std::max(1L, lanes * per_lane)));
+    a.unit_subs = (int32_t)b;
+    a.n_wunits = (int32_t)(((long)a.n_whole + b - 1) / b);
+}
+
+static inline void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_buf, size_t tail_cap) {
+    static const int tail_env = env_int("RT_MK_TAIL", 1);
+    const size_t per_sub = (size_t)std::max(0, a.n_samples) * 3 * sizeof(double);
+    long n_split = 0;
+    if (tail_env && tail_buf && a.n_samples >= 64 && per_sub > 0)
+        n_split = std::min({lanes, nsub / 2, (long)(tail_cap / per_sub)});
+    a.n_whole = (int32_t)(nsub - n_split);
+    // chunks of 2^chunk_lg samples, about RT_MK_TAIL_CPS (4) per subpixel: every chunk costs a
+    // ticket on the one global counter, and short chunks make those atomics the bottleneck of the
+    // tail (16 per subpixel measured 11% slower on the whole frame)
+    // ... and at least 32 samples (≈500 wave iterations): shorter chunks turn over so often that the
+    // counter's atomics saturate (8-sample chunks at 256 spp: the tail ran at a third of the speed)
+    static const int cps_target = std::max(1, env_int("RT_MK_TAIL_CPS", 4));
+    a.chunk_lg = 5;
+    while ((a.n_samples >> a.chunk_lg) > cps_target) ++a.chunk_lg;
+    a.tail_cps = (a.n_samples + (1 << a.chunk_lg) - 1) >> a.chunk_lg;
+    if (a.tail_cps < 2) a.n_whole = (int32_t)nsub;  // nothing to split
+    a.tail_buf = tail_buf;
+    plan_units(a, lanes);
+}
+
+// k_tail_sum_f64 for the split tail of a megakernel launch (render_f64.hip)
+void launch_tail_sum_f64(const RenderArgs& a, double* sub_buf, long n_split, hipStream_t st);
+
+}  // namespace rt

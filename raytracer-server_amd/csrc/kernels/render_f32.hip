@@ -563,7 +563,7 @@ RT_DEV32 long wave_ticket(uint32_t* counter, bool want) {
 // iteration). The subpixel mean is written in f64 for k_finalize_f64 (clamp, gamma, `as u8`).
 template <bool MESH, bool MIS, int W>
 __global__ __launch_bounds__(256, W) void k_megakernel_f32(DevScene sc, RenderArgs a, double* __restrict__ sub_buf,
-                                                       uint32_t* next_sub, long nsub) {
+                                                       uint32_t* next_sub, long nsub, int unit) {
     Cam cam;
     cam.pos = f3((float)sc.cam_pos[0], (float)sc.cam_pos[1], (float)sc.cam_pos[2]);
     cam.dir = f3((float)sc.cam_dir[0], (float)sc.cam_dir[1], (float)sc.cam_dir[2]);
@@ -573,8 +573,12 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f32(DevScene sc, RenderAr
     cam.rh = (float)(1.0 / a.height);
     const float light_pdf = (float)sc.light_pdf;
     uint32_t nverts = 0;
-    long id = wave_ticket(next_sub, true);
-    bool active = id < nsub;
+    // a ticket is a run of `unit` consecutive subpixels (fewer atomics on the one counter at low spp,
+    // render_f64.hip: plan_units)
+    const long nunits = (nsub + unit - 1) / unit;
+    long t0 = wave_ticket(next_sub, true);
+    long id = t0 * unit, end = min(id + unit, nsub);
+    bool active = t0 < nunits;
     int smp = 0;
     F3 acc = f3(0.f, 0.f, 0.f);
     Path ps;
@@ -607,14 +611,22 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f32(DevScene sc, RenderAr
                     o[0] = (double)acc.x * a.inv_n;
                     o[1] = (double)acc.y * a.inv_n;
                     o[2] = (double)acc.z * a.inv_n;
-                    finished = true;
+                    if (++id < end) {  // the next subpixel of the run
+                        smp = 0;
+                        acc = f3(0.f, 0.f, 0.f);
+                        start = true;
+                        nb = false;
+                    } else {
+                        finished = true;
+                    }
                 }
             }
         }
         const long t = wave_ticket(next_sub, finished && !(a.cancel && *(const volatile int32_t*)a.cancel));
         if (finished) {
-            if (t >= 0 && t < nsub) {
-                id = t;
+            if (t >= 0 && t < nunits) {
+                id = t * unit;
+                end = min(id + unit, nsub);
                 smp = 0;
                 acc = f3(0.f, 0.f, 0.f);
                 start = true;
@@ -663,7 +675,9 @@ static hipError_t launch_w(const DevScene& sc, const RenderArgs& a, double* sub_
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
     const long blocks = std::max(1L, std::min((long)ncu * per_cu, (nsub + 255) / 256));
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub, nsub);
+    // about 256 samples per ticket, at least 16 tickets per resident lane (render_f64.hip: plan_units)
+    const long unit = std::max(1L, std::min((long)std::max(1, 256 / std::max(1, a.n_samples)), nsub / (blocks * 256 * 16)));
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub, nsub, (int)unit);
     return hipGetLastError();
 }
 

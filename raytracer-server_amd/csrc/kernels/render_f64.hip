@@ -10,56 +10,11 @@
 
 #include "../device/integrator_f64.h"
 #include "kernels.h"
+#include "megakernel_common.h"
+#include "render_flat_f64.h"
 
 namespace rt {
 using namespace f64;
-
-// Wave-aggregated ticket: every lane with `want` gets the next value of *counter (one atomic per
-// wave). All 64 lanes must call it together.
-__device__ __forceinline__ long wave_ticket(uint32_t* counter, bool want) {
-    const unsigned long long m = __ballot(want);
-    if (m == 0ull) return -1;
-    const int lane = __lane_id();
-    const int leader = __ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-    base = __shfl(base, leader, 64);
-    const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
-    return want ? (long)base + __popcll(below) : -1;
-}
-
-// Adds the wave's vertex counts to *counter and zeroes them. All 64 lanes must call it together.
-__device__ __forceinline__ void flush_count(unsigned long long* counter, uint32_t& n) {
-    if (!counter) return;
-    unsigned long long v = n;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if (__lane_id() == 0 && v) atomicAdd(counter, v);
-    n = 0;
-}
-
-// Work unit of ticket t: subpixel t whole (t < n_whole: samples [0, n)), or chunk c = t - n_whole of
-// the split tail (subpixel n_whole + c / cps, samples [k 2^chunk_lg, (k + 1) 2^chunk_lg), k = c % cps).
-__device__ __forceinline__ void unit_of(const RenderArgs& a, long t, int& id, int& s) {
-    if (t < a.n_whole) {
-        id = (int)t;
-        s = 0;
-    } else {
-        const uint32_t c = (uint32_t)(t - a.n_whole);  // < n_split * cps < 2^32 (plan_tail)
-        const uint32_t q = c / (uint32_t)a.tail_cps;
-        id = a.n_whole + (int)q;
-        s = (int)(c - q * (uint32_t)a.tail_cps) << a.chunk_lg;
-    }
-}
-// Is sample s2 (> s) part of the unit that holds sample s?
-__device__ __forceinline__ bool unit_has(const RenderArgs& a, int id, int s, int s2) {
-    return s2 < a.n_samples && (id < a.n_whole || (s2 >> a.chunk_lg) == (s >> a.chunk_lg));
-}
-// Is sample s + 1 still part of the unit that holds sample s? (No register for the unit's end: a
-// split unit ends at the next multiple of 2^chunk_lg.)
-__device__ __forceinline__ bool unit_has_next(const RenderArgs& a, int id, int s) {
-    return s + 1 < a.n_samples && (id < a.n_whole || ((s + 1) >> a.chunk_lg) == (s >> a.chunk_lg));
-}
 
 // Persistent megakernel: a resident grid whose lanes pull subpixels from a global counter. A lane
 // walks the spp/4 sample paths of its subpixel vertex by vertex; when a path ends, the next sample
@@ -111,10 +66,10 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
     uint32_t nverts = 0;
     // tickets: whole subpixels, then the split tail's chunks (unit_of)
     const long n_split = nsub - a.n_whole;
-    const long nunits = a.n_whole + n_split * a.tail_cps;
-    int id, s;  // subpixel (tile-local, < 2^31: rt_api.cpp check_params) and sample of the unit in hand
+    const long nunits = a.n_wunits + n_split * a.tail_cps;
+    int id, end, s;  // subpixel (tile-local, < 2^31: rt_api.cpp check_params), end of the unit's run, sample
     const long t0 = wave_ticket(next_sub, true);
-    unit_of(a, t0, id, s);
+    unit_of(a, t0, id, end, s);
     bool active = t0 < nunits;
     acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
     PathState ps;
@@ -182,7 +137,14 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
                         o[0] = acc.x;
                         o[1] = acc.y;
                         o[2] = acc.z;
-                        done = true;
+                        if (++id < end) {  // the next subpixel of the run, no ticket
+                            s = 0;
+                            acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
+                            nbuf = 0;
+                            hb = 0;
+                        } else {
+                            done = true;
+                        }
                     }
                 } else {  // split tail: the sample's radiance, summed in order by k_tail_sum_f64
                     double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
@@ -203,7 +165,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
         const long nt = wave_ticket(next_sub, done && !stop);
         if (__any(done)) flush_count(a.counters, nverts);  // keeps the 32-bit lane counts far from overflow
         if (done) {
-            unit_of(a, nt, id, s);
+            unit_of(a, nt, id, end, s);
             active = !stop && nt < nunits;
             acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
             fresh = true;
@@ -216,8 +178,6 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
     flush_count(a.counters, nverts);
     RT_DBG_TFLUSH();
 }
-
-__device__ __forceinline__ bool lane_id_is0() { return __lane_id() == 0; }
 
 // Begins the octree walk of the next candidate mesh after gen slot g (Scene::trace_ray's /
 // mutually_visible's loop over the mesh objects); false when no mesh is left.
@@ -352,6 +312,105 @@ RT_DEV void park_query(const Park& p, const Ray& r, const RayInv& wi, double wt,
     p.I(11) = hobj; p.I(12) = hprim; p.I(13) = -1; p.I(15) = 0;
 }
 
+// One round of walk steps for the queries held by the lanes with `wk` (the query in park `pk`;
+// closest: the closest-hit query of Scene::trace_ray, else the shadow query of mutually_visible):
+// up to ksteps steps, after the first only while >= wmin lanes still walk. Returns, per lane,
+// whether its query finished; the results are then in pk (D16 t, I11 object, I12 prim, I15
+// occluded), otherwise the walk state is stored back into pk.
+template <class C>
+RT_DEV bool walk_round(const DevScene& sc, const Park& pk, const bool wk, const bool closest, int ksteps, int wmin) {
+    bool walking = wk, done = false;
+    if constexpr (C::bvh) {
+      if (__any(walking)) {
+        WalkRegsBvh r;
+        if (walking) park_load_bvh(pk, r);
+        const ParkStack stk{pk};
+        for (int k = 0; k < ksteps && (k == 0 ? __any(walking) : __popcll(__ballot(walking)) >= wmin); ++k) {
+            RT_DBG_WAVE(10, lane_id_is0());
+            RT_DBG_WAVE(11, walking);
+            if (walking) {
+                bool fin = false;
+                if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
+                    const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
+                    fin = !next_mesh_walk_bvh<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w);
+                } else {
+                    const bool shadow = !closest;
+                    const int st = bvh_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, stk, shadow ? r.wt : -1.0);
+                    if (st != WALK_RUN) {
+                        if (!shadow) {
+                            if (st == WALK_HIT) {
+                                HitRec h{r.wt, r.hobj, r.hprim};
+                                consider(h, r.w.bt, tables(sc)->gen_idx[r.g], r.w.best);
+                                r.wt = h.t;
+                                r.hobj = h.obj;
+                                r.hprim = h.prim;
+                            }
+                        } else {
+                            r.occluded = st == WALK_HIT && !(r.w.bt + 0.001 >= r.wt);  // mutually_visible
+                            fin = r.occluded;
+                        }
+                        r.w.cur = -1;  // next step: the next mesh, if any
+                    }
+                }
+                if (fin) {  // results for the vertex phase
+                    walking = false;
+                    done = true;
+                    pk.D(16) = r.wt;
+                    pk.I(11) = r.hobj;
+                    pk.I(12) = r.hprim;
+                    pk.I(15) = r.occluded;
+                }
+            }
+        }
+        if (walking) park_store_bvh(pk, r);
+      }
+    } else if (__any(walking)) {
+        WalkRegs r;
+        if (walking) park_load(pk, r);
+        // up to ksteps steps; after the first, only while at least wmin lanes still walk
+        for (int k = 0; k < ksteps && (k == 0 ? __any(walking) : __popcll(__ballot(walking)) >= wmin); ++k) {
+            RT_DBG_WAVE(10, lane_id_is0());
+            RT_DBG_WAVE(11, walking);
+            if (walking) {
+                bool fin = false;
+                if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
+                    const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
+                    fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w);
+                } else {
+                    double t;
+                    int prim;
+                    const int st = walk_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim);
+                    if (st != WALK_RUN) {
+                        if (closest) {
+                            if (st == WALK_HIT) {
+                                HitRec h{r.wt, r.hobj, r.hprim};
+                                consider(h, t, tables(sc)->gen_idx[r.g], prim);
+                                r.wt = h.t;
+                                r.hobj = h.obj;
+                                r.hprim = h.prim;
+                            }
+                        } else {
+                            r.occluded = st == WALK_HIT && !(t + 0.001 >= r.wt);  // mutually_visible's ERR_MARGIN
+                            fin = r.occluded;
+                        }
+                        r.w.cur = -1;  // next step: the next mesh, if any
+                    }
+                }
+                if (fin) {  // results for the vertex phase
+                    walking = false;
+                    done = true;
+                    pk.D(16) = r.wt;
+                    pk.I(11) = r.hobj;
+                    pk.I(12) = r.hprim;
+                    pk.I(15) = r.occluded;
+                }
+            }
+        }
+        if (walking) park_store(pk, r);
+    }
+    return done;
+}
+
 template <int F, int W>
 __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
                                                                uint32_t* next_sub, long nsub, int ksteps, int wmin,
@@ -383,10 +442,10 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     uint32_t nverts = 0;
     // tickets: whole subpixels, then the split tail's chunks (unit_of), as in k_megakernel_f64
     const long n_split = nsub - a.n_whole;
-    const long nunits = a.n_whole + n_split * a.tail_cps;
-    int id, s;
+    const long nunits = a.n_wunits + n_split * a.tail_cps;
+    int id, end, s;
     const long t0 = wave_ticket(next_sub, true);
-    unit_of(a, t0, id, s);
+    unit_of(a, t0, id, end, s);
     bool active = t0 < nunits;
     acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
     PathState ps;
@@ -394,92 +453,16 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     bool nvalid = false;
     int phase = PH_TRACE;
     bool walking = false, cont = false;
+    RT_DBG_TINIT();
     while (__any(active)) {
         RT_DBG_WAVE(8, lane_id_is0());
-        if constexpr (C::bvh) {
-          if (__any(walking)) {
-            WalkRegsBvh r;
-            if (walking) park_load_bvh(park, r);
-            const ParkStack stk{park};
-            for (int k = 0; k < ksteps && (k == 0 ? __any(walking) : __popcll(__ballot(walking)) >= wmin); ++k) {
-                if (walking) {
-                    bool fin = false;
-                    if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
-                        const double tmax = phase == PH_WALK_CLOSEST ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
-                        fin = !next_mesh_walk_bvh<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w);
-                    } else {
-                        const bool shadow = phase != PH_WALK_CLOSEST;
-                        const int st = bvh_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, stk, shadow ? r.wt : -1.0);
-                        if (st != WALK_RUN) {
-                            if (!shadow) {
-                                if (st == WALK_HIT) {
-                                    HitRec h{r.wt, r.hobj, r.hprim};
-                                    consider(h, r.w.bt, tables(sc)->gen_idx[r.g], r.w.best);
-                                    r.wt = h.t;
-                                    r.hobj = h.obj;
-                                    r.hprim = h.prim;
-                                }
-                            } else {
-                                r.occluded = st == WALK_HIT && !(r.w.bt + 0.001 >= r.wt);  // mutually_visible
-                                fin = r.occluded;
-                            }
-                            r.w.cur = -1;  // next step: the next mesh, if any
-                        }
-                    }
-                    if (fin) {  // results for the vertex phase
-                        walking = false;
-                        park.D(16) = r.wt;
-                        park.I(11) = r.hobj;
-                        park.I(12) = r.hprim;
-                        park.I(15) = r.occluded;
-                    }
-                }
-            }
-            if (walking) park_store_bvh(park, r);
-          }
-        } else if (__any(walking)) {
-            WalkRegs r;
-            if (walking) park_load(park, r);
-            // up to ksteps steps; after the first, only while at least wmin lanes still walk
-            for (int k = 0; k < ksteps && (k == 0 ? __any(walking) : __popcll(__ballot(walking)) >= wmin); ++k) {
-                RT_DBG_WAVE(10, lane_id_is0());
-                RT_DBG_WAVE(11, walking);
-                if (walking) {
-                    bool fin = false;
-                    if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
-                        const double tmax = phase == PH_WALK_CLOSEST ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
-                        fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w);
-                    } else {
-                        double t;
-                        int prim;
-                        const int st = walk_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim);
-                        if (st != WALK_RUN) {
-                            if (phase == PH_WALK_CLOSEST) {
-                                if (st == WALK_HIT) {
-                                    HitRec h{r.wt, r.hobj, r.hprim};
-                                    consider(h, t, tables(sc)->gen_idx[r.g], prim);
-                                    r.wt = h.t;
-                                    r.hobj = h.obj;
-                                    r.hprim = h.prim;
-                                }
-                            } else {
-                                r.occluded = st == WALK_HIT && !(t + 0.001 >= r.wt);  // mutually_visible's ERR_MARGIN
-                                fin = r.occluded;
-                            }
-                            r.w.cur = -1;  // next step: the next mesh, if any
-                        }
-                    }
-                    if (fin) {  // results for the vertex phase
-                        walking = false;
-                        park.D(16) = r.wt;
-                        park.I(11) = r.hobj;
-                        park.I(12) = r.hprim;
-                        park.I(15) = r.occluded;
-                    }
-                }
-            }
-            if (walking) park_store(park, r);
+        RT_DBG_TSTART(t_it);
+        RT_DBG_TSTART(t_wk);
+        if (__any(walking)) {
+            if (walk_round<C>(sc, park, walking, phase == PH_WALK_CLOSEST, ksteps, wmin)) walking = false;
         }
+        RT_DBG_TEND(1, t_wk);
+        RT_DBG_TSTART(t_vx);
         bool done = false;
         RT_DBG_WAVE(9, active && !walking);
         if (active && !walking) {
@@ -537,7 +520,13 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                         o[0] = acc.x;
                         o[1] = acc.y;
                         o[2] = acc.z;
-                        done = true;
+                        if (++id < end) {  // the next subpixel of the run, no ticket
+                            s = 0;
+                            acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
+                            nvalid = false;
+                        } else {
+                            done = true;
+                        }
                     }
                 } else {  // split tail (k_tail_sum_f64)
                     double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
@@ -549,6 +538,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                 }
             }
         }
+        RT_DBG_TEND(2, t_vx);
+        RT_DBG_TSTART(t_bk);
         // camera-sample refill pass: lanes with a path in progress (walking or not) and a next sample
         // in the same unit
         const bool need = active && !fresh && !nvalid && unit_has_next(a, id, s);
@@ -565,14 +556,17 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
         const long nt = wave_ticket(next_sub, done && !stop);
         if (__any(done)) flush_count(a.counters, nverts);  // keeps the 32-bit lane counts far from overflow
         if (done) {
-            unit_of(a, nt, id, s);
+            unit_of(a, nt, id, end, s);
             active = !stop && nt < nunits;
             acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
             fresh = true;
             nvalid = false;
         }
+        RT_DBG_TEND(4, t_bk);
+        RT_DBG_TEND(0, t_it);
     }
     flush_count(a.counters, nverts);
+    RT_DBG_TFLUSH();
 }
 
 // Split tail: subpixel n_whole + j's mean from its samples' radiance, summed in sample order
@@ -630,48 +624,6 @@ __global__ __launch_bounds__(256) void k_trace_f64(DevScene sc, long n, const do
     }
 }
 
-// Resident grid of a persistent kernel: as many 256-thread blocks as fit on the device at once.
-template <class K>
-static long resident_blocks(K kernel, long want) {
-    int dev = 0, ncu = 256, per_cu = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-    return std::max(1L, std::min((long)ncu * per_cu, want));
-}
-
-static int env_int(const char* name, int dflt) {
-    const char* v = std::getenv(name);
-    return v ? std::atoi(v) : dflt;
-}
-
-#ifndef RT_MK_W4
-#define RT_MK_W4 4  // waves/SIMD of the analytic-scene kernel (A/B builds: -DRT_MK_W4=5)
-#endif
-// Split tail (RenderArgs::n_whole): the last subpixels are handed out in chunks of samples, so the
-// frame does not end with lanes idling while others finish a whole subpixel (the 1/N-sized frames
-// of an N-GPU run hold only a few subpixels per lane). Up to one subpixel per resident lane is
-// split, limited by the scratch buffer (tail_cap bytes); RT_MK_TAIL=0 disables it.
-static void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_buf, size_t tail_cap) {
-    static const int tail_env = env_int("RT_MK_TAIL", 1);
-    const size_t per_sub = (size_t)std::max(0, a.n_samples) * 3 * sizeof(double);
-    long n_split = 0;
-    if (tail_env && tail_buf && a.n_samples >= 64 && per_sub > 0)
-        n_split = std::min({lanes, nsub / 2, (long)(tail_cap / per_sub)});
-    a.n_whole = (int32_t)(nsub - n_split);
-    // chunks of 2^chunk_lg samples, about RT_MK_TAIL_CPS (4) per subpixel: every chunk costs a
-    // ticket on the one global counter, and short chunks make those atomics the bottleneck of the
-    // tail (16 per subpixel measured 11% slower on the whole frame)
-    // ... and at least 32 samples (≈500 wave iterations): shorter chunks turn over so often that the
-    // counter's atomics saturate (8-sample chunks at 256 spp: the tail ran at a third of the speed)
-    static const int cps_target = std::max(1, env_int("RT_MK_TAIL_CPS", 4));
-    a.chunk_lg = 5;
-    while ((a.n_samples >> a.chunk_lg) > cps_target) ++a.chunk_lg;
-    a.tail_cps = (a.n_samples + (1 << a.chunk_lg) - 1) >> a.chunk_lg;
-    if (a.tail_cps < 2) a.n_whole = (int32_t)nsub;  // nothing to split
-    a.tail_buf = tail_buf;
-}
-
 template <int F, int W>
 static void launch_mk(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub, long nsub,
                       int refill, double* tail_buf, size_t tail_cap, hipStream_t st) {
@@ -692,8 +644,8 @@ static void launch_mm(const DevScene& sc, const RenderArgs& a_in, double* sub_bu
     const long blocks = resident_blocks(k_megakernel_mesh_f64<F, W>, (nsub + 255) / 256);
     RenderArgs a = a_in;
     plan_tail(a, nsub, blocks * 256, tail_buf, tail_cap);
-    hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub,
-                       nsub, ksteps, wmin, refill);
+    hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf,
+                       next_sub, nsub, ksteps, wmin, refill);
     const long n_split = nsub - a.n_whole;
     if (n_split > 0) {
         const long tb = std::max(1L, std::min(4096L, (n_split + 255) / 256));
@@ -726,9 +678,13 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, dou
     static const int refill = env_int("RT_MK_CAM_REFILL", 24);
     static const int wmin = std::max(1, env_int("RT_MK_WALK_MIN", 1));
     static const int bvh_fused = env_int("RT_MK_BVH_FUSED", 0);  // A/B: nearest-triangle mode without interleaving
+    // scenes whose meshes are all flat octrees (the cubes): block-synchronous batched mesh queries
+    static const int flat = env_int("RT_MK_FLAT", 1);
+    if (flat && a.all_flat && (a.features & 25) == 9)
+        return launch_megakernel_flat_f64(sc, a, sub_buf, next_sub, tail_buf, tail_cap, refill, st);
     if (interleave && (a.features & 9) == 9 && a.mesh_nodes >= interleave && !((a.features & 16) && bvh_fused)) {
-#define RT_MM_CASE(F)                                                        \
-    case F:                                                                  \
+#define RT_MM_CASE(F)                                                                          \
+    case F:                                                                                    \
         launch_mm<F, 2>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, tail_buf, tail_cap, st); \
         break;
         switch (a.features & 31) {
@@ -764,6 +720,12 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, dou
     }
 #undef RT_MK_CASE
     return hipGetLastError();
+}
+
+void launch_tail_sum_f64(const RenderArgs& a, double* sub_buf, long n_split, hipStream_t st) {
+    if (n_split <= 0) return;
+    const long tb = std::max(1L, std::min(4096L, (n_split + 255) / 256));
+    hipLaunchKernelGGL(k_tail_sum_f64, dim3((unsigned)tb), dim3(256), 0, st, a, sub_buf, n_split);
 }
 
 hipError_t launch_finalize_f64(const RenderArgs& a, const double* sub_buf, hipStream_t st) {

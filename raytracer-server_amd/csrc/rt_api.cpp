@@ -292,6 +292,42 @@ void pack_scene(rt_scene* s) {
             }
         }
         if (oc.size() > 0 && oc.kind[0]) dm.root_leaf = leaf_of[0];
+        // flat octree tables (DevMesh::flat): which leaves hold each triangle, leaf lists ascending
+        dm.flat = 0;
+        if (oc.size() > 0 && m.num_triangles() <= (size_t)rt::kFlatMaxTris) {
+            bool ok = true;
+            uint8_t lm[rt::kFlatMaxTris] = {0};
+            auto add_leaf = [&](int32_t node, int bit) {
+                int32_t prev = -1;
+                for (int32_t r = 0; r < oc.leaf_cnt[node]; ++r) {
+                    const int32_t t = oc.refs[oc.leaf_off[node] + r];
+                    ok &= t > prev && t < (int32_t)m.num_triangles();
+                    prev = t;
+                    if (ok) lm[t] |= (uint8_t)(1u << bit);
+                }
+            };
+            if (oc.kind[0]) {
+                dm.flat_root_leaf = 1;
+                dm.flat_kids = 1;
+                add_leaf(0, 0);
+            } else {
+                dm.flat_root_leaf = 0;
+                dm.flat_kids = 0;
+                for (int k = 0; k < 8 && ok; ++k) {
+                    const int32_t c8 = oc.child[k];
+                    if (c8 < 0) continue;
+                    ok &= oc.kind[c8] != 0;  // every child a leaf
+                    if (ok) {
+                        dm.flat_kids |= 1 << k;
+                        add_leaf(c8, k);
+                    }
+                }
+            }
+            if (ok) {
+                dm.flat = 1;
+                for (int j = 0; j < rt::kFlatMaxTris; ++j) dm.flat_leaf[j / 4] |= (uint32_t)lm[j] << (8 * (j % 4));
+            }
+        }
         dm.bvh_base = (int32_t)p.bvh.size();
         dm.btri_base = (int32_t)p.btris.size();
         build_bvh(p, m, dm.tri_base);
@@ -625,6 +661,8 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
         a.features = (s->host.meshes.empty() ? 0 : 1) | (phong ? 2 : 0) | (a.mis ? 4 : 0) | (ds.compact ? 8 : 0);
         if ((p->flags & RT_FLAG_MESH_NEAREST) && !s->host.meshes.empty()) a.features |= 16;
         for (const auto& m : s->host.meshes) a.mesh_nodes = std::max(a.mesh_nodes, (int32_t)m.octree.size());
+        a.all_flat = !s->packed.meshes.empty() && s->packed.meshes.size() <= 4;
+        for (const auto& dm : s->packed.meshes) a.all_flat &= dm.flat != 0;
     }
     a.seed = p->seed;
     rt::host::camera_frame(s->host, p->width, p->height, a.cx, a.cy);

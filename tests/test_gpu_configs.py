@@ -85,7 +85,7 @@ def test_c3_cubes_mis_vs_nee_same_seed(rt, gpu_scenes):
                               "block_ratio_min": float(block.min()), "block_ratio_median": float(np.median(block)),
                               "block_ratio_max": float(block.max()), "K": K, "spp": spp, "size": [w, h]})
     assert np.all(np.abs(diff) <= 4 * se + 1e-12), (diff, se)
-    assert ratio < 1.5
+    assert ratio < 1.0  # measured 0.917 (blocks 0.71 .. 1.00) on the first run, profiles/r02_c3_mis_vs_nee.json
 
 
 C5_W = C5_H = 4096

@@ -13,6 +13,8 @@
 #                    HBM traffic (FETCH_SIZE / WRITE_SIZE), L2 hit rate (TCC_HIT / TCC_MISS), clock
 #                    (GRBM_GUI_ACTIVE) and the SQ instruction mix, each pass a run of its own
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (":" separates args), e.g. py:tools/configs_bench.py:--quick
+#   env:VAR=VAL[,VAR=VAL]  export for the following tasks (A/B of the RT_* switches)
+#   dbgbuild         build the diagnostic library lib/variants/dbg.so (better: build it here and ship it)
 # Env: TAG (output subdirectory, default "run"), BENCH_ARGS (extra bench.py arguments).
 export TMPDIR=/tmp
 TAG=${TAG:-run}
@@ -78,11 +80,22 @@ for task in "$@"; do
         pmc_pass "${key}_sq2" $SQ2 -- "${P[@]}"
         pmc_pass "${key}_sq3" $SQ3 -- "${P[@]}"
         echo "pmc $key ok" ;;
+    dbgbuild)
+        # diagnostic library (RT_DEBUG_COUNTERS + RT_DEBUG_TIMERS) at raytracer-server_amd/lib/variants/dbg.so
+        make -s -j16 -C raytracer-server_amd BUILD=build_dbg LIB=lib/variants/dbg.so \
+            EXTRA="-DRT_DEBUG_COUNTERS=1 -DRT_DEBUG_TIMERS=1" > "$OUT/dbgbuild.log" 2>&1 || fail dbgbuild "$OUT/dbgbuild.log"
+        echo "dbg build ok" ;;
+    env)
+        # env:VAR=VAL[,VAR=VAL...] applies to the tasks after it (A/B runs of the RT_* switches)
+        IFS=, read -r -a KV <<< "${task#env:}"
+        for kv in "${KV[@]}"; do export "$kv"; echo "env $kv"; done ;;
     py)
         script=${A[1]}
-        timeout -k 10 900 python -u "$script" "${A[@]:2}" > "$OUT/$(basename "$script" .py).log" 2>&1 \
-            || fail "$script" "$OUT/$(basename "$script" .py).log"
-        tail -40 "$OUT/$(basename "$script" .py).log" ;;
+        LOG="$OUT/$(basename "$script" .py).log"
+        echo "== $task $(env | grep -E '^RT_' | tr '\n' ' ')" >> "$LOG"
+        timeout -k 10 900 python -u "$script" "${A[@]:2}" > "$OUT/py_last.log" 2>&1 || { cat "$OUT/py_last.log" >> "$LOG"; fail "$script" "$OUT/py_last.log"; }
+        cat "$OUT/py_last.log" >> "$LOG"
+        tail -40 "$OUT/py_last.log" ;;
     *)
         fail "unknown task $task" ;;
     esac

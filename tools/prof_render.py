@@ -19,7 +19,7 @@ mis = "mis" in sys.argv[6:]
 nearest = "nearest" in sys.argv[6:]  # RT_FLAG_MESH_NEAREST (BVH)
 s = rt_amd.Scene.from_toml(os.path.join(REPO, "scenes", f"{scene}.toml"))
 kw = dict(megakernel=(mode == "mk"), mis=mis, mesh_nearest=nearest, fp32=(mode == "f32"))
-rt_amd.render(s, 64, 48, 4, **kw)  # warm-up
+rt_amd.render(s, w, h, 4, **kw)  # warm-up at the same size (buffers allocated and touched)
 t = time.perf_counter()
 rgb, _, st = rt_amd.render(s, w, h, spp, **kw)
 dt = time.perf_counter() - t
