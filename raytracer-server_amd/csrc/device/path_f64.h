@@ -480,6 +480,11 @@ __shared__ unsigned long long s_dbg_time[4 * 16];
 // Each walk_step does one unit of work (a triangle test, a backtrack, or a child pick that either
 // opens a leaf or descends and masks the new node's children), so a wave can interleave walks of
 // different lengths and refill lanes whose walk ended (persistent traversal kernels).
+#ifndef RT_LTRI_INDEX
+#define RT_LTRI_INDEX 0  // 1: leaf triangle lists as indices into DevScene::tris instead of per-leaf copies
+                         // (3.6 MB instead of 18 MB for the unicorn, but one more dependent load per
+                         // triangle: measured 3% slower)
+#endif
 struct OctWalk {
     double mn[3], mx[3];  // box of `cur`
     int32_t cur, depth;
@@ -569,7 +574,12 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
             if (w.lpos < w.lend) {
                 RT_DBG(4);
                 double tt;
-                if (tri_t(sc.ltris[w.lpos], ray, &tt) && (w.best < 0 || tt < w.bt)) {
+#if RT_LTRI_INDEX
+                const DevTri& tr = sc.tris[sc.ltri_id[w.lpos]];  // leaf list = triangle indices (3.6 MB table)
+#else
+                const DevTri& tr = sc.ltris[w.lpos];  // leaf list = triangle copies (18 MB for the unicorn)
+#endif
+                if (tri_t(tr, ray, &tt) && (w.best < 0 || tt < w.bt)) {
                     w.bt = tt;
                     w.best = w.lpos;
                 }

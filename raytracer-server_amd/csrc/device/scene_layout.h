@@ -72,7 +72,7 @@ struct alignas(16) DevBvhNode {
 constexpr int32_t kKidEmpty = -1;
 RT_LAYOUT_FN int32_t kid_leaf(int32_t leaf) { return -2 - leaf; }
 // node_up[node] = {parent node (-1 at the root), octant slot in the parent}
-// leaf_span[leaf] = {first leaf triangle (index into ltris), count}
+// leaf_span[leaf] = {first entry of the leaf in ltri_id (ltris in RT_LTRI_INDEX=0 builds), count}
 
 // Triangle, precomputed exactly as Triangle::intersect derives it per call (geometry.rs:637-653):
 // a, ab = b - a, ac = c - a, n = ((c - a) x (b - a)).norm(). 12 doubles = 96 B.
@@ -138,9 +138,10 @@ struct DevScene {
     const int32_t* node_kids;   // [node][8], see kid_leaf
     const int2* node_up;        // [node] {parent, slot}
     const int2* leaf_span;      // [leaf] {first ltri, count}
-    const DevTri* ltris;        // leaf triangle lists as copies, in leaf order (the reference's leaves hold
-                                // (index, Triangle) copies too, geometry.rs:1131-1137)
-    const int32_t* ltri_id;     // [ltri] global triangle index (the hit's `prim`)
+    const DevTri* ltris;        // RT_LTRI_INDEX=0 builds only: leaf triangle lists as copies, in leaf order
+                                // (the reference's leaves hold (index, Triangle) copies, geometry.rs:1131-1137)
+    const int32_t* ltri_id;     // [ltri] leaf triangle lists as global triangle indices into `tris`, in leaf
+                                // order (the walk's triangles and the hit's `prim`)
     const DevTri* tris;         // per triangle (surface normal, mesh-light sampling)
     const double* tri_cum_area;  // per triangle, cumulative area within its mesh (mesh-light pick)
     const CompactTab* ctab;     // compact tables (valid when `compact`; see Cfg::compact)

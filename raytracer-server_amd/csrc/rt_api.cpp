@@ -19,6 +19,10 @@
 #include "kernels/kernels.h"
 #include "kernels/wavefront.h"
 
+#ifndef RT_LTRI_INDEX
+#define RT_LTRI_INDEX 0  // as path_f64.h (1: leaf triangle lists as indices, no per-leaf copies uploaded)
+#endif
+
 namespace {
 
 thread_local std::string g_err;
@@ -284,10 +288,12 @@ void pack_scene(rt_scene* s) {
         for (size_t i = 0; i < oc.size(); ++i) {
             if (!oc.kind[i]) continue;
             leaf_of[i] = (int32_t)p.leaves.size();
-            p.leaves.push_back(int2{(int32_t)p.ltris.size(), oc.leaf_cnt[i]});
+            p.leaves.push_back(int2{(int32_t)p.ltri_id.size(), oc.leaf_cnt[i]});
             for (int32_t r = 0; r < oc.leaf_cnt[i]; ++r) {
                 const int32_t t = oc.refs[oc.leaf_off[i] + r];
+#if !RT_LTRI_INDEX
                 p.ltris.push_back(p.tris[dm.tri_base + t]);
+#endif
                 p.ltri_id.push_back(dm.tri_base + t);
             }
         }
