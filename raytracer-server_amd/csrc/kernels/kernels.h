@@ -32,7 +32,7 @@ struct RenderArgs {
     const int32_t* cancel;         // optional device view of the host cancel flag (mapped memory)
     double* tail_buf;              // split-tail sample radiance (see n_whole)
     int32_t f32_brute;             // f32 mode: meshes of <= f32_brute triangles are tested without the BVH
-    int32_t all_flat;              // every mesh is a flat octree (DevMesh::flat) and there are <= 4 of them
+    int32_t all_flat;              // every mesh is a flat octree (DevMesh::flat) and there are <= 2 of them
 };
 
 // tail_buf / tail_cap: scratch for the split tail (bytes); the launcher sizes the tail to fit it.

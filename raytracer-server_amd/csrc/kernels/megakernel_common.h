@@ -52,6 +52,12 @@ __device__ __forceinline__ void unit_of(const RenderArgs& a, long t, int& id, in
         s = (int)(c - q * (uint32_t)a.tail_cps) << a.chunk_lg;
     }
 }
+// One past the last subpixel of the run of whole subpixels that holds subpixel id (< n_whole): runs
+// are aligned to unit_subs, so no register holds the run's end (the analytic megakernel's VGPRs).
+__device__ __forceinline__ int run_end(const RenderArgs& a, int id) {
+    const int b = a.unit_subs;
+    return min((id / b + 1) * b, a.n_whole);
+}
 // Is sample s2 (> s) part of the unit that holds sample s?
 __device__ __forceinline__ bool unit_has(const RenderArgs& a, int id, int s, int s2) {
     return s2 < a.n_samples && (id < a.n_whole || (s2 >> a.chunk_lg) == (s >> a.chunk_lg));

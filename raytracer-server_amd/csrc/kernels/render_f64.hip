@@ -67,9 +67,12 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
     // tickets: whole subpixels, then the split tail's chunks (unit_of)
     const long n_split = nsub - a.n_whole;
     const long nunits = a.n_wunits + n_split * a.tail_cps;
-    int id, end, s;  // subpixel (tile-local, < 2^31: rt_api.cpp check_params), end of the unit's run, sample
+    int id, s;  // subpixel (tile-local, < 2^31: rt_api.cpp check_params) and sample of the unit in hand
     const long t0 = wave_ticket(next_sub, true);
-    unit_of(a, t0, id, end, s);
+    {
+        int end_unused;  // the run's end is recomputed when needed (run_end)
+        unit_of(a, t0, id, end_unused, s);
+    }
     bool active = t0 < nunits;
     acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
     PathState ps;
@@ -137,7 +140,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
                         o[0] = acc.x;
                         o[1] = acc.y;
                         o[2] = acc.z;
-                        if (++id < end) {  // the next subpixel of the run, no ticket
+                        if (id + 1 < run_end(a, id)) {  // the next subpixel of the run, no ticket
+                            ++id;
                             s = 0;
                             acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
                             nbuf = 0;
@@ -165,7 +169,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
         const long nt = wave_ticket(next_sub, done && !stop);
         if (__any(done)) flush_count(a.counters, nverts);  // keeps the 32-bit lane counts far from overflow
         if (done) {
-            unit_of(a, nt, id, end, s);
+            int end_unused;
+            unit_of(a, nt, id, end_unused, s);
             active = !stop && nt < nunits;
             acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
             fresh = true;

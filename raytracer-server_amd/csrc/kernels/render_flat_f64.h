@@ -4,17 +4,20 @@
 // In the per-lane megakernels a mesh query (the octree walk of Mesh::intersect, geometry.rs:883-905,
 // 1237-1295) is needed by ~6% of the lanes per trace, but almost every wave has one such lane, so
 // every wave pays for the walk with 1-4 lanes active (lane utilisation 0.22 on the cubes). Here the
-// 4 waves of a block run each path vertex in lockstep phases separated by barriers:
-//   A  camera / analytic closest hit (planes, spheres); lanes whose ray may reach a mesh queue a
+// 4 waves of a block advance their paths one vertex per iteration in three phases separated by two
+// barriers:
+//   A  camera / analytic closest hit (planes, spheres); a lane whose ray may reach a mesh queues a
 //      closest-hit query per mesh in LDS;
-//   B  the block's queued queries are processed densely, one lane per query, one wave per mesh chunk
-//      of 64: flat_query evaluates the walk's result from every triangle of that mesh (scalar loads:
-//      all lanes of a chunk query the same mesh);
-//   C  the lane merges the mesh hits in Scene::trace_ray's order (ties to the lower object index),
-//      shades the vertex; a shadow ray the analytic objects let through is queued per mesh;
-//   D  shadow queries as in B;
-//   E  the NEE term is added unless a mesh blocks the shadow ray (mutually_visible); sample and
-//      subpixel bookkeeping, tickets.
+//   P  every query the block queued is processed densely, one lane per query and one wave per chunk
+//      of up to 64 queries of one mesh and kind: the closest-hit queries of this vertex and the
+//      shadow queries of the previous one (so the 4 waves share up to 4 chunks); flat_query evaluates
+//      the walk's result from every triangle of that mesh (scalar loads: a chunk's lanes query the
+//      same mesh);
+//   C  the previous vertex's shadow results: its NEE term is added unless a mesh blocks the shadow
+//      ray (mutually_visible); this vertex: the mesh hits merged in Scene::trace_ray's order (ties to
+//      the lower object index), shading, and a shadow ray the analytic objects let through queued per
+//      mesh for the next P; sample / subpixel bookkeeping and tickets. A path that ends with a shadow
+//      query pending waits one iteration (no new path in A) until C has its result.
 // Every query returns the same bits as the per-lane walk (same tri_t, same box_hit per octant, same
 // visiting order), so frames are identical to k_megakernel_f64's and the wavefront's (tested).
 // Included by render_f64.hip (one code object: the diagnostic counters of path_f64.h are per code
@@ -34,7 +37,7 @@ using namespace f64;
 
 namespace {
 
-constexpr int kFlatMeshes = 4;  // meshes of a flat scene (LDS queues)
+constexpr int kFlatMeshes = 2;  // meshes of a flat scene (LDS queues; rt_api.cpp: RenderArgs::all_flat)
 constexpr int kBlk = 256;
 typedef __attribute__((address_space(3))) double LdsD;
 typedef __attribute__((address_space(3))) uint64_t LdsU;
@@ -124,28 +127,41 @@ RT_DEV void enqueue(int32_t* cnt, int32_t* queue, bool want) {
     }
 }
 
-// Phase B / D: the block's queued queries of round r, chunks of 64 entries of one mesh handed to
-// the waves in turn; results to s_rt / s_rp [mesh][lane].
-RT_DEV void process_queries(const DevScene& sc, const int32_t* cnt, const int32_t* queue, const LdsD* q,
-                            double* rt, int32_t* rp) {
+// Phase P: the block's queued queries, chunks of up to 64 entries of one (kind, mesh) handed to the
+// waves in turn. Kind 0: closest-hit queries (ray in qc), results t / prim to rt / rp [mesh][lane];
+// kind 1: shadow queries (ray + |y - x| in qs), result occluded to ro [mesh][lane]
+// (mutually_visible: the walk's hit t with t + 0.001 < |y - x|).
+RT_DEV void process_queries(const DevScene& sc, const int32_t* cnt_c, const int32_t* queue_c, const int32_t* cnt_s,
+                            const int32_t* queue_s, const LdsD* qc, const LdsD* qs, double* rt, int32_t* rp,
+                            int32_t* ro) {
     const int wv = threadIdx.x >> 6, ln = __lane_id();
     int ci = 0;
-    for (int m = 0; m < sc.n_meshes; ++m) {
-        const int c = cnt[m];
-        for (int k = 0; k * 64 < c; ++k, ++ci) {
-            if ((ci & 3) != wv) continue;
-            const int e = k * 64 + ln;
-            RT_DBG_WAVE(13, lane_id_is0());
-            RT_DBG_WAVE(12, e < c);
-            if (e < c) {
-                const int who = queue[m * kBlk + e];
-                const Ray r{v3(q[who], q[kBlk + who], q[2 * kBlk + who]), v3(q[3 * kBlk + who], q[4 * kBlk + who], q[5 * kBlk + who])};
-                const RayInv inv = make_inv(r.d);
-                double t = 0.0;
-                int prim = -1;
-                const bool hit = flat_query(sc, sc.meshes[m], r, inv, &t, &prim);
-                rt[m * kBlk + who] = t;
-                rp[m * kBlk + who] = hit ? prim : -1;
+    for (int kind = 0; kind < 2; ++kind) {
+        const int32_t* cnt = kind ? cnt_s : cnt_c;
+        const int32_t* queue = kind ? queue_s : queue_c;
+        const LdsD* q = kind ? qs : qc;
+        for (int m = 0; m < sc.n_meshes; ++m) {
+            const int c = cnt[m];
+            for (int k = 0; k * 64 < c; ++k, ++ci) {
+                if ((ci & 3) != wv) continue;
+                const int e = k * 64 + ln;
+                RT_DBG_WAVE(13, lane_id_is0());
+                RT_DBG_WAVE(12, e < c);
+                if (e < c) {
+                    const int who = queue[m * kBlk + e];
+                    const Ray r{v3(q[who], q[kBlk + who], q[2 * kBlk + who]),
+                                v3(q[3 * kBlk + who], q[4 * kBlk + who], q[5 * kBlk + who])};
+                    const RayInv inv = make_inv(r.d);
+                    double t = 0.0;
+                    int prim = -1;
+                    const bool hit = flat_query(sc, sc.meshes[m], r, inv, &t, &prim);
+                    if (kind == 0) {
+                        rt[m * kBlk + who] = t;
+                        rp[m * kBlk + who] = hit ? prim : -1;
+                    } else {
+                        ro[m * kBlk + who] = hit && !(t + 0.001 >= q[6 * kBlk + who]) ? 1 : 0;
+                    }
+                }
             }
         }
     }
@@ -155,7 +171,7 @@ RT_DEV void process_queries(const DevScene& sc, const int32_t* cnt, const int32_
 
 template <int F, int W>
 __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
-                                                                uint32_t* next_sub, long nsub, int refill) {
+                                                                uint32_t* next_sub, long nsub) {
     using C = Cfg<F>;
     static_assert(C::mesh && C::compact && !C::bvh, "flat-mesh kernel: compact scenes, octree meshes");
     DevScene sc = sc_g;
@@ -167,22 +183,19 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
         for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
         sc.objects = s_objs;
     }
-    // per lane (one column per thread): subpixel accumulator, one-deep camera-sample buffer
-    __shared__ double s_acc[3 * kBlk], s_nbd[3 * kBlk];
-    __shared__ uint64_t s_nbr[2 * kBlk];
-    LdsD* acc_l = (LdsD*)s_acc + threadIdx.x;
-    LdsD* nbd = (LdsD*)s_nbd + threadIdx.x;
-    LdsU* nbr = (LdsU*)s_nbr + threadIdx.x;
-    // the lane's query ray (origin, direction) for the processing lane, results per (mesh, lane), and
-    // the per-mesh queues of the closest (0) and shadow (1) rounds
-    __shared__ double s_q[6 * kBlk];
+    // per lane (one column per thread): subpixel accumulator; the closest-hit query ray (o, d), the
+    // shadow query ray (o, d, |y - x|); results per (mesh, lane); queues per (kind, parity, mesh):
+    // the closest queries of iteration i and the shadow queries of i - 1 are in flight together
+    __shared__ double s_acc[3 * kBlk];
+    __shared__ double s_qc[6 * kBlk], s_qs[7 * kBlk];
     __shared__ double s_rt[kFlatMeshes * kBlk];
-    __shared__ int32_t s_rp[kFlatMeshes * kBlk];
-    __shared__ int32_t s_queue[kFlatMeshes * kBlk];
-    __shared__ int32_t s_cnt[2][kFlatMeshes];
+    __shared__ int32_t s_rp[kFlatMeshes * kBlk], s_ro[kFlatMeshes * kBlk];
+    __shared__ int32_t s_queue[2][2][kFlatMeshes * kBlk];  // [kind][parity]
+    __shared__ int32_t s_cnt[2][2][kFlatMeshes];
     __shared__ int32_t s_active;
+    LdsD* acc_l = (LdsD*)s_acc + threadIdx.x;
     const int tid = threadIdx.x;
-    if (tid < 2 * kFlatMeshes) s_cnt[tid / kFlatMeshes][tid % kFlatMeshes] = 0;
+    if (tid < 4 * kFlatMeshes) (&s_cnt[0][0][0])[tid] = 0;
     if (tid == 0) s_active = 0;
     RT_DBG_TINIT();
     __syncthreads();
@@ -200,76 +213,75 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
     }
     acc_l[0] = 0.0; acc_l[kBlk] = 0.0; acc_l[2 * kBlk] = 0.0;
     PathState ps;
-    bool fresh = true, nvalid = false;
+    bool fresh = true;
+    bool pend = false;     // a shadow query of the last vertex is in flight
+    bool waiting = false;  // the last vertex ended the sample; it is finished once its shadow result is in
+    V3 pc = v3(0, 0, 0);   // that query's NEE term, added unless a mesh blocks the shadow ray
+    uint32_t smask = 0;    // meshes the shadow query was queued for
     __syncthreads();
-    for (;;) {
+    for (int it = 0;; ++it) {
+        const int par = it & 1;
         RT_DBG_WAVE(8, lane_id_is0());
         RT_DBG_WAVE(9, active);
         RT_DBG_TSTART(t_a);
         // ---------------- A: camera, analytic closest hit, closest-hit queries
-        if (tid < kFlatMeshes) s_cnt[1][tid] = 0;  // shadow round's queues (read in D of the last iteration)
-        if (active && fresh && nvalid) {
-            begin_path(sc, CameraSample{v3(nbd[0], nbd[kBlk], nbd[2 * kBlk]), nbr[0], nbr[kBlk]}, ps);
+        const bool go = active && !waiting;
+        if (go && fresh) {
+            begin_sample(sc, a, subpixel_of(a, id), s, ps);
             fresh = false;
-            nvalid = false;
-        }
-        {
-            // camera pass: lanes starting a path now, plus buffer refills once >= refill lanes need one
-            const bool now = active && fresh;
-            const bool need = active && !fresh && !nvalid && unit_has_next(a, id, s);
-            if (__any(now) || (refill > 0 && __popcll(__ballot(need)) >= refill)) {
-                if (now || (refill > 0 && need)) {
-                    const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), now ? s : s + 1);
-                    if (now) {
-                        begin_path(sc, nb, ps);
-                        fresh = false;
-                    } else {
-                        nbd[0] = nb.d.x; nbd[kBlk] = nb.d.y; nbd[2 * kBlk] = nb.d.z;
-                        nbr[0] = nb.r0; nbr[kBlk] = nb.r1;
-                        nvalid = true;
-                    }
-                }
-            }
         }
         HitRec h{0.0, -1, -1};
         RayInv inv{};
         double tmax = INFINITY;
-        if (active) {
+        if (go) {
             inv = make_inv(ps.ray.d);
             h = trace_analytic<C>(sc, ps.ray, inv);
             tmax = h.obj >= 0 ? h.t : INFINITY;
-            s_q[tid] = ps.ray.o.x; s_q[kBlk + tid] = ps.ray.o.y; s_q[2 * kBlk + tid] = ps.ray.o.z;
-            s_q[3 * kBlk + tid] = ps.ray.d.x; s_q[4 * kBlk + tid] = ps.ray.d.y; s_q[5 * kBlk + tid] = ps.ray.d.z;
+            s_qc[tid] = ps.ray.o.x; s_qc[kBlk + tid] = ps.ray.o.y; s_qc[2 * kBlk + tid] = ps.ray.o.z;
+            s_qc[3 * kBlk + tid] = ps.ray.d.x; s_qc[4 * kBlk + tid] = ps.ray.d.y; s_qc[5 * kBlk + tid] = ps.ray.d.z;
         }
         uint32_t qmask = 0;
         for (int m = 0; m < sc.n_meshes; ++m) {
             const DevMesh& M = sc.meshes[m];
-            const bool want = active && near_box(M.cull_box, ps.ray, inv, M.cull_pad, tmax);
+            const bool want = go && near_box(M.cull_box, ps.ray, inv, M.cull_pad, tmax);
             qmask |= want ? (1u << m) : 0u;
-            enqueue(&s_cnt[0][m], s_queue + m * kBlk, want);
+            enqueue(&s_cnt[0][par][m], s_queue[0][par] + m * kBlk, want);
         }
         RT_DBG_TEND(1, t_a);
         RT_DBG_TSTART(t_w1);
         __syncthreads();
         RT_DBG_TEND(6, t_w1);
-        if (s_active == 0) break;  // every lane of the block is done (stable between E and the next A)
-        // ---------------- B: closest-hit queries
-        RT_DBG_TSTART(t_b);
-        process_queries(sc, s_cnt[0], s_queue, (const LdsD*)s_q, s_rt, s_rp);
-        RT_DBG_TEND(2, t_b);
+        if (s_active == 0) break;  // every lane of the block is done (stable between C and the next A)
+        // ---------------- P: this vertex's closest-hit queries, the previous vertex's shadow queries
+        RT_DBG_TSTART(t_p);
+        process_queries(sc, s_cnt[0][par], s_queue[0][par], s_cnt[1][par ^ 1], s_queue[1][par ^ 1], (const LdsD*)s_qc,
+                        (const LdsD*)s_qs, s_rt, s_rp, s_ro);
+        RT_DBG_TEND(2, t_p);
         RT_DBG_TSTART(t_w2);
         __syncthreads();
         RT_DBG_TEND(6, t_w2);
         RT_DBG_TSTART(t_c);
-        // ---------------- C: merge the mesh hits, shade, shadow queries
-        if (tid < kFlatMeshes) s_cnt[0][tid] = 0;
-        bool cont = false, pend = false;
-        V3 pc = v3(0, 0, 0);
-        double dist = 0.0;
-        uint32_t smask = 0;
+        // ---------------- C: shadow results, merge + shade, shadow queries, bookkeeping
+        if (tid < kFlatMeshes) s_cnt[0][par][tid] = 0;            // next appended in A of iteration it + 2
+        else if (tid < 2 * kFlatMeshes) s_cnt[1][par ^ 1][tid - kFlatMeshes] = 0;  // in C of it + 1
+        bool finish = false;  // the sample of this lane's path is complete
+        if (pend) {
+            bool occluded = false;
+            for (int m = 0; m < sc.n_meshes; ++m)
+                if ((smask >> m) & 1u) occluded |= s_ro[m * kBlk + tid] != 0;
+            if (!occluded) ps.L = ps.L + pc;
+            pend = false;
+            if (waiting) {
+                waiting = false;
+                finish = true;
+            }
+        }
+        smask = 0;
+        bool want_s = false;
         Ray sr{v3(0, 0, 0), v3(0, 0, 1)};
         RayInv sinv{};
-        if (active) {
+        double dist = 0.0;
+        if (go) {
             CTab* T = tables(sc);
             for (int g = 0; g < T->n_gen; ++g) {  // Scene::trace_ray's loop over the meshes (ties: lower index)
                 const int idx = T->gen_idx[g];
@@ -282,75 +294,63 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
             nverts += h.obj >= 0;
             ShadowDefer df;
             df.pending = false;
-            cont = shade_vertex<C>(sc, a, ps, h, &df);
+            const bool cont = shade_vertex<C>(sc, a, ps, h, &df);
             if (df.pending) {  // the analytic objects let the shadow ray through; a mesh may block it
                 pend = true;
                 pc = df.c;
                 dist = df.dist;
                 sr = Ray{df.o, df.d};
                 sinv = make_inv(sr.d);
-                s_q[tid] = sr.o.x; s_q[kBlk + tid] = sr.o.y; s_q[2 * kBlk + tid] = sr.o.z;
-                s_q[3 * kBlk + tid] = sr.d.x; s_q[4 * kBlk + tid] = sr.d.y; s_q[5 * kBlk + tid] = sr.d.z;
+                s_qs[tid] = sr.o.x; s_qs[kBlk + tid] = sr.o.y; s_qs[2 * kBlk + tid] = sr.o.z;
+                s_qs[3 * kBlk + tid] = sr.d.x; s_qs[4 * kBlk + tid] = sr.d.y; s_qs[5 * kBlk + tid] = sr.d.z;
+                s_qs[6 * kBlk + tid] = dist;
+            }
+            if (!cont) {
+                if (pend) waiting = true;  // finished in the next C
+                else finish = true;
             }
         }
         for (int m = 0; m < sc.n_meshes; ++m) {
             const DevMesh& M = sc.meshes[m];
-            const bool want = pend && near_box(M.cull_box, sr, sinv, M.cull_pad, dist);
+            const bool want = pend && go && near_box(M.cull_box, sr, sinv, M.cull_pad, dist);
             smask |= want ? (1u << m) : 0u;
-            enqueue(&s_cnt[1][m], s_queue + m * kBlk, want);
+            enqueue(&s_cnt[1][par][m], s_queue[1][par] + m * kBlk, want);
+            want_s |= want;
         }
-        RT_DBG_TEND(3, t_c);
-        RT_DBG_TSTART(t_w3);
-        __syncthreads();
-        RT_DBG_TEND(6, t_w3);
-        // ---------------- D: shadow queries
-        RT_DBG_TSTART(t_d);
-        process_queries(sc, s_cnt[1], s_queue, (const LdsD*)s_q, s_rt, s_rp);
-        RT_DBG_TEND(4, t_d);
-        RT_DBG_TSTART(t_w4);
-        __syncthreads();
-        RT_DBG_TEND(6, t_w4);
-        RT_DBG_TSTART(t_e);
-        // ---------------- E: visibility, sample / subpixel bookkeeping, tickets
-        bool done = false;
-        if (active) {
-            if (pend) {
-                bool occluded = false;  // mutually_visible (scene.rs:258-270): t + 0.001 < |y - x|
-                for (int m = 0; m < sc.n_meshes; ++m) {
-                    if ((smask >> m) & 1u) {
-                        const int p = s_rp[m * kBlk + tid];
-                        occluded |= p >= 0 && !(s_rt[m * kBlk + tid] + 0.001 >= dist);
-                    }
-                }
-                if (!occluded) ps.L = ps.L + pc;
+        if (go && pend && !want_s) {  // no mesh near the shadow segment: unblocked now
+            ps.L = ps.L + pc;
+            pend = false;
+            if (waiting) {
+                waiting = false;
+                finish = true;
             }
-            if (!cont) {
-                fresh = true;
-                if (id < a.n_whole) {
-                    V3 acc = v3(acc_l[0], acc_l[kBlk], acc_l[2 * kBlk]);
-                    acc = acc + ps.L * a.inv_n;  // server.rs:357-358
-                    acc_l[0] = acc.x; acc_l[kBlk] = acc.y; acc_l[2 * kBlk] = acc.z;
-                    if (++s == a.n_samples) {
-                        double* o = sub_buf + (size_t)id * 3;
-                        o[0] = acc.x;
-                        o[1] = acc.y;
-                        o[2] = acc.z;
-                        if (++id < end) {  // the next subpixel of the run, no ticket
-                            s = 0;
-                            acc_l[0] = 0.0; acc_l[kBlk] = 0.0; acc_l[2 * kBlk] = 0.0;
-                            nvalid = false;
-                        } else {
-                            done = true;
-                        }
+        }
+        bool done = false;
+        if (finish) {
+            fresh = true;
+            if (id < a.n_whole) {
+                V3 acc = v3(acc_l[0], acc_l[kBlk], acc_l[2 * kBlk]);
+                acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                acc_l[0] = acc.x; acc_l[kBlk] = acc.y; acc_l[2 * kBlk] = acc.z;
+                if (++s == a.n_samples) {
+                    double* o = sub_buf + (size_t)id * 3;
+                    o[0] = acc.x;
+                    o[1] = acc.y;
+                    o[2] = acc.z;
+                    if (++id < end) {  // the next subpixel of the run, no ticket
+                        s = 0;
+                        acc_l[0] = 0.0; acc_l[kBlk] = 0.0; acc_l[2 * kBlk] = 0.0;
+                    } else {
+                        done = true;
                     }
-                } else {  // split tail (k_tail_sum_f64)
-                    double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
-                    o[0] = ps.L.x;
-                    o[1] = ps.L.y;
-                    o[2] = ps.L.z;
-                    done = !unit_has_next(a, id, s);
-                    ++s;
                 }
+            } else {  // split tail (k_tail_sum_f64)
+                double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
+                o[0] = ps.L.x;
+                o[1] = ps.L.y;
+                o[2] = ps.L.z;
+                done = !unit_has_next(a, id, s);
+                ++s;
             }
         }
         bool stop = false;
@@ -364,13 +364,12 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
             ended = !active;
             acc_l[0] = 0.0; acc_l[kBlk] = 0.0; acc_l[2 * kBlk] = 0.0;
             fresh = true;
-            nvalid = false;
         }
         {
             const unsigned long long m = __ballot(ended);
             if (__lane_id() == 0 && m) atomicSub(&s_active, __popcll(m));
         }
-        RT_DBG_TEND(5, t_e);
+        RT_DBG_TEND(3, t_c);
     }
     flush_count(a.counters, nverts);
     RT_DBG_TFLUSH();
@@ -378,11 +377,11 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
 
 template <int F, int W>
 static void launch_flat(const DevScene& sc, RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
-                        double* tail_buf, size_t tail_cap, int refill, hipStream_t st) {
+                        double* tail_buf, size_t tail_cap, hipStream_t st) {
     const long blocks = resident_blocks(k_megakernel_flat_f64<F, W>, (nsub + kBlk - 1) / kBlk);
     plan_tail(a, nsub, blocks * kBlk, tail_buf, tail_cap);
     hipLaunchKernelGGL((k_megakernel_flat_f64<F, W>), dim3((unsigned)blocks), dim3(kBlk), 0, st, sc, a, sub_buf,
-                       next_sub, nsub, refill);
+                       next_sub, nsub);
 }
 
 // The flat-mesh megakernel (scenes whose meshes are all DevMesh::flat; octree mode).
@@ -394,8 +393,8 @@ hipError_t launch_megakernel_flat_f64(const DevScene& sc, const RenderArgs& a_in
     static const int waves = env_int("RT_MK_FLAT_WAVES", 3);
 #define RT_FLAT_CASE(F)                                                                       \
     case F:                                                                                   \
-        if (waves == 2) launch_flat<F, 2>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, refill, st); \
-        else launch_flat<F, 3>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, refill, st); \
+        if (waves == 2) launch_flat<F, 2>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, st); \
+        else launch_flat<F, 3>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, st); \
         break;
     switch (a.features & 15) {
         RT_FLAT_CASE(9) RT_FLAT_CASE(11) RT_FLAT_CASE(13) RT_FLAT_CASE(15)

@@ -667,7 +667,7 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
         a.features = (s->host.meshes.empty() ? 0 : 1) | (phong ? 2 : 0) | (a.mis ? 4 : 0) | (ds.compact ? 8 : 0);
         if ((p->flags & RT_FLAG_MESH_NEAREST) && !s->host.meshes.empty()) a.features |= 16;
         for (const auto& m : s->host.meshes) a.mesh_nodes = std::max(a.mesh_nodes, (int32_t)m.octree.size());
-        a.all_flat = !s->packed.meshes.empty() && s->packed.meshes.size() <= 4;
+        a.all_flat = !s->packed.meshes.empty() && s->packed.meshes.size() <= 2;  // render_flat_f64.h: kFlatMeshes
         for (const auto& dm : s->packed.meshes) a.all_flat &= dm.flat != 0;
     }
     a.seed = p->seed;

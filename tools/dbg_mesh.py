@@ -32,8 +32,8 @@ print(f"  wave iterations {c[8]}: vertex-phase lanes/iteration {c[9] / it:.1f}, 
 T = {0: "iteration", 1: "walk phase", 2: "vertex phase", 4: "refill + ticket", 7: "surface()", 9: "light_sample",
      10: "visible()", 11: "brdf_sample", 13: "trace: inv + planes", 14: "trace: spheres"}
 if os.environ.get("RT_MK_FLAT", "1") != "0" and scene == "cubes":  # render_flat_f64.hip phases
-    T.update({1: "A camera + analytic", 2: "B closest queries", 3: "C merge + shade", 4: "D shadow queries",
-              5: "E visibility + bookkeeping", 6: "barrier waits"})
+    T.update({1: "A camera + analytic", 2: "P mesh queries", 3: "C shadow results + shade + bookkeeping",
+              6: "barrier waits"})
     print(f"  flat kernel: query chunks/iteration {c[13] / it:.2f}, lanes per chunk {c[12] / max(1, c[13]):.1f}, "
           f"active lanes/iteration {c[9] / it:.1f}")
 tot = max(1, r[32] or sum(r[33:48]))

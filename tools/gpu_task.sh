@@ -61,7 +61,7 @@ for task in "$@"; do
         B=(python bench.py --steps 1 --warmup 0 --no-cpu-baseline $BENCH_ARGS)
         pmc_pass bench_fetch FETCH_SIZE -- "${B[@]}"
         pmc_pass bench_write WRITE_SIZE -- "${B[@]}"
-        key=$(tail -1 "$OUT/bench_fetch.log" | python -c "import json,sys;d=json.loads(sys.stdin.read());print(d['config']['workload'],d['config']['mode'])")
+        key=$(grep '^{"metric"' "$OUT/bench_fetch.log" | tail -1 | python -c "import json,sys;d=json.loads(sys.stdin.read());print(d['config']['workload'],d['config']['mode'])")
         python tools/pmc_traffic.py "$OUT/bench_fetch/run_counter_collection.csv" "$OUT/bench_write/run_counter_collection.csv" \
             "$key" --out "$OUT/pmc_traffic.json" || fail benchpmc ;;
     configs)
