@@ -628,9 +628,15 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
     const int32_t c = sc.node_kids[8 * (size_t)w.cur + oi];
     if (c <= -2) {  // open a leaf
         RT_DBG(3);
-        const int2 ls = sc.leaf_span[-2 - c];
-        w.lpos = ls.x;
-        w.lend = ls.x + ls.y;
+        const int32_t e = -2 - c;  // the leaf's range inline (kid_leaf), or its id behind the escape count
+        int32_t first = e >> 6, cnt = e & 63;
+        if (cnt == kKidCountEscape) {
+            const int2 ls = sc.leaf_span[first];
+            first = ls.x;
+            cnt = ls.y;
+        }
+        w.lpos = first;
+        w.lend = first + cnt;
         w.best = -1;
         return WALK_RUN;
     }

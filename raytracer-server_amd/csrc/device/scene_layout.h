@@ -68,9 +68,16 @@ struct alignas(16) DevBvhNode {
     int32_t a, count, axis, pad;
 };
 
-// node_kids[node][8] entries: -1 empty octant, >= 0 parent node, <= -2 leaf id (-2 - entry).
+// node_kids[node][8] entries: -1 empty octant, >= 0 parent node, <= -2 a leaf: e = -2 - entry holds
+// the leaf's triangle range inline, first list entry (e >> 6) and count (e & 63), so opening a leaf
+// needs no further load; a leaf of >= 63 triangles or a first entry >= 2^25 stores count 63 and its
+// leaf id in e >> 6 instead (its range is then read from leaf_span).
 constexpr int32_t kKidEmpty = -1;
-RT_LAYOUT_FN int32_t kid_leaf(int32_t leaf) { return -2 - leaf; }
+constexpr int32_t kKidCountEscape = 63;
+RT_LAYOUT_FN int32_t kid_leaf(int32_t leaf, int32_t first, int32_t count) {
+    const bool inl = count < kKidCountEscape && first < (1 << 25);
+    return -2 - ((inl ? first : leaf) << 6 | (inl ? count : kKidCountEscape));
+}
 // node_up[node] = {parent node (-1 at the root), octant slot in the parent}
 // leaf_span[leaf] = {first entry of the leaf in ltri_id (ltris in RT_LTRI_INDEX=0 builds), count}
 
@@ -135,7 +142,7 @@ struct Compact32 {
 struct DevScene {
     const DevObject* objects;
     const DevMesh* meshes;
-    const int32_t* node_kids;   // [node][8], see kid_leaf
+    const int32_t* node_kids;   // [node][8], see kid_leaf (leaf triangle ranges inline)
     const int2* node_up;        // [node] {parent, slot}
     const int2* leaf_span;      // [leaf] {first ltri, count}
     const DevTri* ltris;        // RT_LTRI_INDEX=0 builds only: leaf triangle lists as copies, in leaf order

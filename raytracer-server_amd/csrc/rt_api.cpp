@@ -342,7 +342,9 @@ void pack_scene(rt_scene* s) {
             p.up.push_back(int2{oc.parent[i] >= 0 ? oc.parent[i] + dm.node_base : -1, oc.slot[i]});
             for (int k = 0; k < 8; ++k) {
                 const int32_t c8 = oc.child[8 * i + k];
-                p.kids.push_back(c8 < 0 ? rt::kKidEmpty : oc.kind[c8] ? rt::kid_leaf(leaf_of[c8]) : c8 + dm.node_base);
+                p.kids.push_back(c8 < 0 ? rt::kKidEmpty
+                                 : oc.kind[c8] ? rt::kid_leaf(leaf_of[c8], p.leaves[leaf_of[c8]].x, p.leaves[leaf_of[c8]].y)
+                                               : c8 + dm.node_base);
             }
         }
         p.meshes.push_back(dm);
