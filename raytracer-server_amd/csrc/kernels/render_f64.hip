@@ -416,10 +416,165 @@ RT_DEV bool walk_round(const DevScene& sc, const Park& pk, const bool wk, const 
     return done;
 }
 
-template <int F, int W>
+// Walk pool (P = true): the walk queries of a block go through one LDS work queue instead of being
+// walked by the lane that owns the path. A wave takes up to 64 runnable queries from the queue (any
+// owner's), walks them for `ksteps` steps, hands finished results to their owners (status word) and
+// puts unfinished queries back. Walk steps then run with the block's queries packed into full waves
+// instead of the ~27 walking lanes of the wave that owns them (the deep octree's walks are 0-40
+// steps long and needed by ~20% of the vertices). The queue holds each query at most
+// once and a block has at most 256 queries (one per path), so a 256-entry ring cannot overflow.
+// Entries are written after the tail is advanced; a taker waits for its entry (-1 = not yet written).
+struct WalkPool {
+    int32_t* ring;      // LDS [256]
+    uint32_t* head;     // LDS: next entry to take
+    uint32_t* tail;     // LDS: next entry to fill
+    uint8_t* status;    // LDS [256] per owner column: 0 closest query, 1 shadow query, 2 done
+};
+enum : uint8_t { POOL_CLOSEST = 0, POOL_SHADOW = 1, POOL_DONE = 2 };
+// Puts column q of every lane with `put` into the queue. All lanes of the wave call.
+RT_DEV void pool_put(const WalkPool& wp, bool put, int32_t q) {
+    const unsigned long long m = __ballot(put);
+    if (m == 0ull) return;
+    const int lane = __lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = __hip_atomic_fetch_add(wp.tail, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    base = __shfl(base, leader, 64);
+    const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+    if (put) __hip_atomic_store(&wp.ring[(base + (uint32_t)__popcll(below)) & 255u], q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Takes up to 64 queries, but only if at least `need` are queued; returns this lane's column or -1.
+// All lanes of the wave call.
+RT_DEV int32_t pool_take(const WalkPool& wp, int need) {
+    uint32_t h = 0, k = 0;
+    if (__lane_id() == 0) {
+        for (;;) {
+            h = __hip_atomic_load(wp.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t t = __hip_atomic_load(wp.tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t avail = t - h;
+            if ((int)avail < max(need, 1)) { k = 0; break; }
+            k = min(avail, 64u);
+            uint32_t exp = h;
+            if (__hip_atomic_compare_exchange_strong(wp.head, &exp, h + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP))
+                break;
+        }
+    }
+    h = __shfl(h, 0, 64);
+    k = __shfl(k, 0, 64);
+    int32_t q = -1;
+    if ((uint32_t)__lane_id() < k) {
+        int32_t* e = &wp.ring[(h + (uint32_t)__lane_id()) & 255u];
+        while ((q = __hip_atomic_load(e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < 0) __builtin_amdgcn_s_sleep(1);
+        __hip_atomic_store(e, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return q;
+}
+
+// Refill: every lane with `want` takes one queued query while any are left (-1 otherwise). All
+// lanes of the wave call.
+constexpr int kPoolRefill = 8;  // refill only when at least this many lanes of the round are idle
+RT_DEV int32_t pool_take_some(const WalkPool& wp, bool want) {
+    const unsigned long long m = __ballot(want);
+    const int lane = __lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t h = 0, k = 0;
+    if (lane == leader) {
+        for (;;) {
+            h = __hip_atomic_load(wp.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t t = __hip_atomic_load(wp.tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            k = min(t - h, (uint32_t)__popcll(m));
+            if (k == 0) break;
+            uint32_t exp = h;
+            if (__hip_atomic_compare_exchange_strong(wp.head, &exp, h + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP))
+                break;
+        }
+    }
+    h = __shfl(h, leader, 64);
+    k = __shfl(k, leader, 64);
+    const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+    const uint32_t rank = (uint32_t)__popcll(below);
+    int32_t q = -1;
+    if (want && rank < k) {
+        int32_t* e = &wp.ring[(h + rank) & 255u];
+        while ((q = __hip_atomic_load(e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < 0) __builtin_amdgcn_s_sleep(1);
+        __hip_atomic_store(e, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return q;
+}
+
+// One pool round: up to ksteps walk steps over queries taken from the pool; a lane whose query
+// finishes hands the result to its owner and, while steps remain, takes the next queued query
+// (refill: the round keeps its lanes full). Unfinished queries go back to the pool. All lanes call.
+template <class C>
+RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d, LdsInt* park_i, int need,
+                       int ksteps) {
+    int32_t q = pool_take(wp, need);
+    if (!__any(q >= 0)) return false;
+    WalkRegs r;
+    bool closest = false;
+    auto col = [&](int32_t c) { return Park{park_d + c, park_i + c}; };
+    if (q >= 0) {
+        park_load(col(q), r);
+        closest = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == POOL_CLOSEST;
+    }
+    for (int k = 0; k < ksteps; ++k) {
+        RT_DBG_WAVE(10, lane_id_is0());
+        RT_DBG_WAVE(11, q >= 0);
+        if (q >= 0) {
+            bool fin = false;
+            if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
+                const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
+                fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w);
+            } else {
+                double t;
+                int prim;
+                const int st = walk_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim);
+                if (st != WALK_RUN) {
+                    if (closest) {
+                        if (st == WALK_HIT) {
+                            HitRec h{r.wt, r.hobj, r.hprim};
+                            consider(h, t, tables(sc)->gen_idx[r.g], prim);
+                            r.wt = h.t;
+                            r.hobj = h.obj;
+                            r.hprim = h.prim;
+                        }
+                    } else {
+                        r.occluded = st == WALK_HIT && !(t + 0.001 >= r.wt);  // mutually_visible's ERR_MARGIN
+                        fin = r.occluded;
+                    }
+                    r.w.cur = -1;  // next step: the next mesh, if any
+                }
+            }
+            if (fin) {  // results for the owner's vertex phase, then the status word
+                const Park pq = col(q);
+                pq.D(16) = r.wt;
+                pq.I(11) = r.hobj;
+                pq.I(12) = r.hprim;
+                pq.I(15) = r.occluded;
+                __hip_atomic_store(&wp.status[q], (uint8_t)POOL_DONE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                q = -1;
+            }
+        }
+        if (k + 1 < ksteps && __popcll(__ballot(q < 0)) >= kPoolRefill) {
+            const int32_t q2 = pool_take_some(wp, q < 0);
+            if (q2 >= 0) {
+                q = q2;
+                park_load(col(q), r);
+                closest = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == POOL_CLOSEST;
+            }
+        }
+    }
+    if (q >= 0) park_store(col(q), r);
+    pool_put(wp, q >= 0, q);
+    return true;
+}
+
+template <int F, int W, bool P>
 __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
                                                                uint32_t* next_sub, long nsub, int ksteps, int wmin,
-                                                               int refill) {
+                                                               int refill, int pool_min, int pool_vmin) {
     using C = Cfg<F>;
     static_assert(C::mesh && C::compact, "mesh megakernel needs the compact tables");
     // object table in LDS, as in k_megakernel_f64 (2 blocks per CU: 2 x 78 KB of LDS)
@@ -438,6 +593,15 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     __shared__ double s_park_d[kParkD * kParkThreads];
     __shared__ int32_t s_park_i[kParkI * kParkThreads];
     const Park park{(LdsDouble*)s_park_d + threadIdx.x, (LdsInt*)s_park_i + threadIdx.x};
+    __shared__ int32_t s_ring[P ? 256 : 1];
+    __shared__ uint8_t s_status[P ? 256 : 1];
+    __shared__ uint32_t s_qhead, s_qtail;
+    const WalkPool wp{s_ring, &s_qhead, &s_qtail, s_status};
+    if constexpr (P) {
+        s_ring[threadIdx.x] = -1;
+        if (threadIdx.x == 0) { s_qhead = 0; s_qtail = 0; }
+        __syncthreads();
+    }
     // subpixel accumulator and camera-sample buffer in LDS, as in k_megakernel_f64
     __shared__ double s_acc[3 * 256], s_nbd[3 * 256];
     __shared__ uint64_t s_nbr[2 * 256];
@@ -463,24 +627,40 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
         RT_DBG_WAVE(8, lane_id_is0());
         RT_DBG_TSTART(t_it);
         RT_DBG_TSTART(t_wk);
-        if (__any(walking)) {
+        bool took = false;
+        if constexpr (P) {
+            // take queued queries (at least pool_min of them while this wave has paths to shade)
+            const int ready = __popcll(__ballot(active && !walking));
+            took = pool_round<C>(sc, wp, (LdsDouble*)s_park_d, (LdsInt*)s_park_i, ready ? pool_min : 1, ksteps);
+            if (!took && !ready) {
+                __builtin_amdgcn_s_sleep(2);  // every path of this wave waits on walks other waves hold
+            }
+            if (walking && __hip_atomic_load(&s_status[threadIdx.x], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == POOL_DONE)
+                walking = false;
+        } else if (__any(walking)) {
             if (walk_round<C>(sc, park, walking, phase == PH_WALK_CLOSEST, ksteps, wmin)) walking = false;
         }
         RT_DBG_TEND(1, t_wk);
         RT_DBG_TSTART(t_vx);
         bool done = false;
-        RT_DBG_WAVE(9, active && !walking);
-        if (active && !walking) {
-            bool shade_now = false, sample_end = false;
+        const bool was_walking = walking;
+        // pool: after a walk round, shade only once pool_vmin paths are ready (denser vertex phases)
+        const bool vphase = !P || !took || __popcll(__ballot(active && !walking)) >= pool_vmin;
+        RT_DBG_WAVE(9, vphase && active && !walking);
+        if (vphase && active && !walking) {
+            bool shade_now = false, sample_end = false, trace_now = true;
             HitRec h;
-            if (phase == PH_WALK_SHADOW) {
+            if (phase == PH_WALK_SHADOW) {  // the shadow result, then (path going on) the next trace
                 if (!park.I(15)) ps.L = ps.L + v3(park.D(17), park.D(18), park.D(19));
                 phase = PH_TRACE;
                 sample_end = !cont;
+                trace_now = cont;
             } else if (phase == PH_WALK_CLOSEST) {
                 h = HitRec{park.D(16), park.I(11), park.I(12)};
                 shade_now = true;
-            } else {
+                trace_now = false;
+            }
+            if (trace_now) {
                 if (fresh) {
                     if (nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[256], nbd[512]), nbr[0], nbr[256]}, ps);
                     else begin_sample(sc, a, subpixel_of(a, id), s, ps);
@@ -491,6 +671,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                 h = trace_analytic<C>(sc, ps.ray, wi);
                 if (mesh_candidate<C>(sc, ps.ray, wi, h.obj >= 0 ? h.t : INFINITY)) {
                     park_query(park, ps.ray, wi, h.t, h.obj, h.prim);
+                    if constexpr (P) s_status[threadIdx.x] = POOL_CLOSEST;
                     phase = PH_WALK_CLOSEST;
                     walking = true;
                 } else {
@@ -509,6 +690,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                     park.D(17) = df.c.x;
                     park.D(18) = df.c.y;
                     park.D(19) = df.c.z;
+                    if constexpr (P) s_status[threadIdx.x] = POOL_SHADOW;
                     phase = PH_WALK_SHADOW;
                     walking = true;
                 }
@@ -543,6 +725,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                 }
             }
         }
+        if constexpr (P) pool_put(wp, walking && !was_walking, (int32_t)threadIdx.x);
         RT_DBG_TEND(2, t_vx);
         RT_DBG_TSTART(t_bk);
         // camera-sample refill pass: lanes with a path in progress (walking or not) and a next sample
@@ -643,14 +826,15 @@ static void launch_mk(const DevScene& sc, const RenderArgs& a_in, double* sub_bu
         hipLaunchKernelGGL(k_tail_sum_f64, dim3((unsigned)tb), dim3(256), 0, st, a, sub_buf, n_split);
     }
 }
-template <int F, int W>
+template <int F, int W, bool P>
 static void launch_mm(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub, long nsub,
-                      int ksteps, int wmin, int refill, double* tail_buf, size_t tail_cap, hipStream_t st) {
-    const long blocks = resident_blocks(k_megakernel_mesh_f64<F, W>, (nsub + 255) / 256);
+                      int ksteps, int wmin, int refill, int pool_min, int pool_vmin, double* tail_buf, size_t tail_cap,
+                      hipStream_t st) {
+    const long blocks = resident_blocks(k_megakernel_mesh_f64<F, W, P>, (nsub + 255) / 256);
     RenderArgs a = a_in;
     plan_tail(a, nsub, blocks * 256, tail_buf, tail_cap);
-    hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf,
-                       next_sub, nsub, ksteps, wmin, refill);
+    hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W, P>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf,
+                       next_sub, nsub, ksteps, wmin, refill, pool_min, pool_vmin);
     const long n_split = nsub - a.n_whole;
     if (n_split > 0) {
         const long tb = std::max(1L, std::min(4096L, (n_split + 255) / 256));
@@ -688,14 +872,25 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, dou
     if (flat && a.all_flat && (a.features & 25) == 9)
         return launch_megakernel_flat_f64(sc, a, sub_buf, next_sub, tail_buf, tail_cap, refill, st);
     if (interleave && (a.features & 9) == 9 && a.mesh_nodes >= interleave && !((a.features & 16) && bvh_fused)) {
+        // octree walks through the block's walk pool (RT_MK_POOL=0: each lane walks its own query)
+        static const int pool = env_int("RT_MK_POOL", 1);
+        static const int pool_min = env_int("RT_MK_POOL_MIN", 32);
+        static const int pool_ksteps = std::max(1, env_int("RT_MK_POOL_KSTEPS", 6));
+        static const int pool_vmin = env_int("RT_MK_POOL_VMIN", 0);
 #define RT_MM_CASE(F)                                                                          \
     case F:                                                                                    \
-        launch_mm<F, 2>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, tail_buf, tail_cap, st); \
+        if (pool) launch_mm<F, 2, true>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
+        else launch_mm<F, 2, false>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, 0, 0, tail_buf, tail_cap, st); \
+        break;
+#define RT_MMB_CASE(F)                                                                         \
+    case F:                                                                                    \
+        launch_mm<F, 2, false>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, 0, 0, tail_buf, tail_cap, st); \
         break;
         switch (a.features & 31) {
             RT_MM_CASE(9) RT_MM_CASE(11) RT_MM_CASE(13) RT_MM_CASE(15)
-            RT_MM_CASE(25) RT_MM_CASE(27) RT_MM_CASE(29) RT_MM_CASE(31)  // nearest-triangle meshes: BVH walks
+            RT_MMB_CASE(25) RT_MMB_CASE(27) RT_MMB_CASE(29) RT_MMB_CASE(31)  // nearest-triangle meshes: BVH walks
         }
+#undef RT_MMB_CASE
 #undef RT_MM_CASE
         return hipGetLastError();
     }
