@@ -70,6 +70,80 @@ __device__ __forceinline__ bool unit_has_next(const RenderArgs& a, int id, int s
 
 __device__ __forceinline__ bool lane_id_is0() { return __lane_id() == 0; }
 
+// Multi-producer multi-consumer work queue of int entries (>= 0) in LDS, shared by the waves of a
+// block without barriers: a ring of mask + 1 entries (initialised to -1) with monotonically growing
+// head / tail counters. The caller guarantees that no more than mask + 1 entries are ever queued
+// at once (each query of a block is in the queue at most once). Entries are written after the tail
+// is advanced, so a taker waits for its entry to turn non-negative; it then resets it to -1.
+struct LdsQueue {
+    int32_t* ring;
+    uint32_t* head;  // next entry to take
+    uint32_t* tail;  // next entry to fill
+    uint32_t mask;   // capacity - 1 (a power of two)
+};
+__device__ __forceinline__ uint32_t queue_len(const LdsQueue& q) {
+    return __hip_atomic_load(q.tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) -
+           __hip_atomic_load(q.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Appends v of every lane with `put` (wave-aggregated). All lanes of the wave call.
+__device__ __forceinline__ void queue_put(const LdsQueue& q, bool put, int32_t v) {
+    const unsigned long long m = __ballot(put);
+    if (m == 0ull) return;
+    const int lane = __lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = __hip_atomic_fetch_add(q.tail, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    base = __shfl(base, leader, 64);
+    const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+    if (put) __hip_atomic_store(&q.ring[(base + (uint32_t)__popcll(below)) & q.mask], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Claims up to `most` entries, but only if at least max(need, 1) are queued; the leader lane does the
+// compare-and-swap. Returns the first claimed position and the count (wave-uniform).
+__device__ __forceinline__ void queue_claim(const LdsQueue& q, int leader, uint32_t most, int need, uint32_t& h, uint32_t& k) {
+    h = 0;
+    k = 0;
+    if (__lane_id() == leader) {
+        for (;;) {
+            h = __hip_atomic_load(q.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t t = __hip_atomic_load(q.tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t avail = t - h;
+            if ((int)avail < max(need, 1)) { k = 0; break; }
+            k = min(avail, most);
+            uint32_t exp = h;
+            if (__hip_atomic_compare_exchange_strong(q.head, &exp, h + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP))
+                break;
+        }
+    }
+    h = __shfl(h, leader, 64);
+    k = __shfl(k, leader, 64);
+}
+__device__ __forceinline__ int32_t queue_read(const LdsQueue& q, uint32_t pos) {
+    int32_t* e = &q.ring[pos & q.mask];
+    int32_t v;
+    while ((v = __hip_atomic_load(e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < 0) __builtin_amdgcn_s_sleep(1);
+    __hip_atomic_store(e, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return v;
+}
+// Takes up to 64 entries (lane i the i-th), but only if at least `need` are queued; -1 for lanes
+// without one. All lanes of the wave call.
+__device__ __forceinline__ int32_t queue_take(const LdsQueue& q, int need) {
+    uint32_t h, k;
+    queue_claim(q, 0, 64u, need, h, k);
+    return (uint32_t)__lane_id() < k ? queue_read(q, h + (uint32_t)__lane_id()) : -1;
+}
+// Every lane with `want` takes one entry while any are queued (-1 otherwise). All lanes call.
+__device__ __forceinline__ int32_t queue_take_each(const LdsQueue& q, bool want) {
+    const unsigned long long m = __ballot(want);
+    if (m == 0ull) return -1;
+    const int lane = __lane_id();
+    uint32_t h, k;
+    queue_claim(q, __ffsll((long long)m) - 1, (uint32_t)__popcll(m), 1, h, k);
+    const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+    const uint32_t rank = (uint32_t)__popcll(below);
+    return want && rank < k ? queue_read(q, h + rank) : -1;
+}
+
 // Resident grid of a persistent kernel: as many 256-thread blocks as fit on the device at once.
 template <class K>
 static inline long resident_blocks(K kernel, long want) {

@@ -416,93 +416,20 @@ RT_DEV bool walk_round(const DevScene& sc, const Park& pk, const bool wk, const 
     return done;
 }
 
-// Walk pool (P = true): the walk queries of a block go through one LDS work queue instead of being
-// walked by the lane that owns the path. A wave takes up to 64 runnable queries from the queue (any
-// owner's), walks them for `ksteps` steps, hands finished results to their owners (status word) and
-// puts unfinished queries back. Walk steps then run with the block's queries packed into full waves
-// instead of the ~27 walking lanes of the wave that owns them (the deep octree's walks are 0-40
-// steps long and needed by ~20% of the vertices). The queue holds each query at most
-// once and a block has at most 256 queries (one per path), so a 256-entry ring cannot overflow.
-// Entries are written after the tail is advanced; a taker waits for its entry (-1 = not yet written).
+// Walk pool (P = true): the walk queries of a block go through one LDS work queue (LdsQueue,
+// megakernel_common.h) instead of being walked by the lane that owns the path. A wave takes up to 64
+// runnable queries from the queue (any owner's), walks them for `ksteps` steps, hands finished
+// results to their owners (status word) and puts unfinished queries back. Walk steps then run with
+// the block's queries packed into full waves instead of the ~27 walking lanes of the wave that owns
+// them (the deep octree's walks are 0-40 steps long and needed by ~20% of the vertices, DESIGN.md
+// §5). The queue holds each query at most once and a block has at most 256 queries (one per path),
+// so a 256-entry ring cannot overflow.
 struct WalkPool {
-    int32_t* ring;      // LDS [256]
-    uint32_t* head;     // LDS: next entry to take
-    uint32_t* tail;     // LDS: next entry to fill
+    LdsQueue q;
     uint8_t* status;    // LDS [256] per owner column: 0 closest query, 1 shadow query, 2 done
 };
 enum : uint8_t { POOL_CLOSEST = 0, POOL_SHADOW = 1, POOL_DONE = 2 };
-// Puts column q of every lane with `put` into the queue. All lanes of the wave call.
-RT_DEV void pool_put(const WalkPool& wp, bool put, int32_t q) {
-    const unsigned long long m = __ballot(put);
-    if (m == 0ull) return;
-    const int lane = __lane_id();
-    const int leader = __ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = __hip_atomic_fetch_add(wp.tail, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    base = __shfl(base, leader, 64);
-    const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
-    if (put) __hip_atomic_store(&wp.ring[(base + (uint32_t)__popcll(below)) & 255u], q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// Takes up to 64 queries, but only if at least `need` are queued; returns this lane's column or -1.
-// All lanes of the wave call.
-RT_DEV int32_t pool_take(const WalkPool& wp, int need) {
-    uint32_t h = 0, k = 0;
-    if (__lane_id() == 0) {
-        for (;;) {
-            h = __hip_atomic_load(wp.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const uint32_t t = __hip_atomic_load(wp.tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const uint32_t avail = t - h;
-            if ((int)avail < max(need, 1)) { k = 0; break; }
-            k = min(avail, 64u);
-            uint32_t exp = h;
-            if (__hip_atomic_compare_exchange_strong(wp.head, &exp, h + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP))
-                break;
-        }
-    }
-    h = __shfl(h, 0, 64);
-    k = __shfl(k, 0, 64);
-    int32_t q = -1;
-    if ((uint32_t)__lane_id() < k) {
-        int32_t* e = &wp.ring[(h + (uint32_t)__lane_id()) & 255u];
-        while ((q = __hip_atomic_load(e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < 0) __builtin_amdgcn_s_sleep(1);
-        __hip_atomic_store(e, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    return q;
-}
-
-// Refill: every lane with `want` takes one queued query while any are left (-1 otherwise). All
-// lanes of the wave call.
 constexpr int kPoolRefill = 8;  // refill only when at least this many lanes of the round are idle
-RT_DEV int32_t pool_take_some(const WalkPool& wp, bool want) {
-    const unsigned long long m = __ballot(want);
-    const int lane = __lane_id();
-    const int leader = __ffsll((long long)m) - 1;
-    uint32_t h = 0, k = 0;
-    if (lane == leader) {
-        for (;;) {
-            h = __hip_atomic_load(wp.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const uint32_t t = __hip_atomic_load(wp.tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            k = min(t - h, (uint32_t)__popcll(m));
-            if (k == 0) break;
-            uint32_t exp = h;
-            if (__hip_atomic_compare_exchange_strong(wp.head, &exp, h + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP))
-                break;
-        }
-    }
-    h = __shfl(h, leader, 64);
-    k = __shfl(k, leader, 64);
-    const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
-    const uint32_t rank = (uint32_t)__popcll(below);
-    int32_t q = -1;
-    if (want && rank < k) {
-        int32_t* e = &wp.ring[(h + rank) & 255u];
-        while ((q = __hip_atomic_load(e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < 0) __builtin_amdgcn_s_sleep(1);
-        __hip_atomic_store(e, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    return q;
-}
 
 // One pool round: up to ksteps walk steps over queries taken from the pool; a lane whose query
 // finishes hands the result to its owner and, while steps remain, takes the next queued query
@@ -510,7 +437,7 @@ RT_DEV int32_t pool_take_some(const WalkPool& wp, bool want) {
 template <class C>
 RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d, LdsInt* park_i, int need,
                        int ksteps) {
-    int32_t q = pool_take(wp, need);
+    int32_t q = queue_take(wp.q, need);
     if (!__any(q >= 0)) return false;
     WalkRegs r;
     bool closest = false;
@@ -558,7 +485,7 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
             }
         }
         if (k + 1 < ksteps && __popcll(__ballot(q < 0)) >= kPoolRefill) {
-            const int32_t q2 = pool_take_some(wp, q < 0);
+            const int32_t q2 = queue_take_each(wp.q, q < 0);
             if (q2 >= 0) {
                 q = q2;
                 park_load(col(q), r);
@@ -567,7 +494,7 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
         }
     }
     if (q >= 0) park_store(col(q), r);
-    pool_put(wp, q >= 0, q);
+    queue_put(wp.q, q >= 0, q);
     return true;
 }
 
@@ -596,7 +523,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     __shared__ int32_t s_ring[P ? 256 : 1];
     __shared__ uint8_t s_status[P ? 256 : 1];
     __shared__ uint32_t s_qhead, s_qtail;
-    const WalkPool wp{s_ring, &s_qhead, &s_qtail, s_status};
+    const WalkPool wp{LdsQueue{s_ring, &s_qhead, &s_qtail, 255u}, s_status};
     if constexpr (P) {
         s_ring[threadIdx.x] = -1;
         if (threadIdx.x == 0) { s_qhead = 0; s_qtail = 0; }
@@ -725,7 +652,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                 }
             }
         }
-        if constexpr (P) pool_put(wp, walking && !was_walking, (int32_t)threadIdx.x);
+        if constexpr (P) queue_put(wp.q, walking && !was_walking, (int32_t)threadIdx.x);
         RT_DBG_TEND(2, t_vx);
         RT_DBG_TSTART(t_bk);
         // camera-sample refill pass: lanes with a path in progress (walking or not) and a next sample

@@ -127,15 +127,47 @@ RT_DEV void enqueue(int32_t* cnt, int32_t* queue, bool want) {
     }
 }
 
-// Phase P: the block's queued queries, chunks of up to 64 entries of one (kind, mesh) handed to the
-// waves in turn. Kind 0: closest-hit queries (ray in qc), results t / prim to rt / rp [mesh][lane];
-// kind 1: shadow queries (ray + |y - x| in qs), result occluded to ro [mesh][lane]
-// (mutually_visible: the walk's hit t with t + 0.001 < |y - x|).
+// Phase P: the block's queued queries in chunks of up to 64 entries of one mesh, handed to the waves
+// in turn (starting at wave `first`). A mesh's entries are its closest-hit queries (ray in qc;
+// results t / prim to rt / rp [mesh][lane]) followed by its shadow queries (ray + |y - x| in qs;
+// result occluded to ro [mesh][lane], mutually_visible: the walk's hit t with t + 0.001 < |y - x|):
+// flat_query is the same for both, so one chunk serves both kinds.
+#ifndef RT_FLAT_MERGE_KINDS
+#define RT_FLAT_MERGE_KINDS 1
+#endif
 RT_DEV void process_queries(const DevScene& sc, const int32_t* cnt_c, const int32_t* queue_c, const int32_t* cnt_s,
                             const int32_t* queue_s, const LdsD* qc, const LdsD* qs, double* rt, int32_t* rp,
-                            int32_t* ro) {
+                            int32_t* ro, int first) {
     const int wv = threadIdx.x >> 6, ln = __lane_id();
-    int ci = 0;
+    int ci = first;
+#if RT_FLAT_MERGE_KINDS
+    for (int m = 0; m < sc.n_meshes; ++m) {
+        const int nc = cnt_c[m], c = nc + cnt_s[m];
+        for (int k = 0; k * 64 < c; ++k, ++ci) {
+            if ((ci & 3) != wv) continue;
+            const int e = k * 64 + ln;
+            RT_DBG_WAVE(13, lane_id_is0());
+            RT_DBG_WAVE(12, e < c);
+            if (e < c) {
+                const int kind = e >= nc;
+                const int who = kind ? queue_s[m * kBlk + e - nc] : queue_c[m * kBlk + e];
+                const LdsD* q = kind ? qs : qc;
+                const Ray r{v3(q[who], q[kBlk + who], q[2 * kBlk + who]),
+                            v3(q[3 * kBlk + who], q[4 * kBlk + who], q[5 * kBlk + who])};
+                const RayInv inv = make_inv(r.d);
+                double t = 0.0;
+                int prim = -1;
+                const bool hit = flat_query(sc, sc.meshes[m], r, inv, &t, &prim);
+                if (kind == 0) {
+                    rt[m * kBlk + who] = t;
+                    rp[m * kBlk + who] = hit ? prim : -1;
+                } else {
+                    ro[m * kBlk + who] = hit && !(t + 0.001 >= q[6 * kBlk + who]) ? 1 : 0;
+                }
+            }
+        }
+    }
+#else
     for (int kind = 0; kind < 2; ++kind) {
         const int32_t* cnt = kind ? cnt_s : cnt_c;
         const int32_t* queue = kind ? queue_s : queue_c;
@@ -165,6 +197,7 @@ RT_DEV void process_queries(const DevScene& sc, const int32_t* cnt_c, const int3
             }
         }
     }
+#endif
 }
 
 }  // namespace
@@ -255,7 +288,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
         // ---------------- P: this vertex's closest-hit queries, the previous vertex's shadow queries
         RT_DBG_TSTART(t_p);
         process_queries(sc, s_cnt[0][par], s_queue[0][par], s_cnt[1][par ^ 1], s_queue[1][par ^ 1], (const LdsD*)s_qc,
-                        (const LdsD*)s_qs, s_rt, s_rp, s_ro);
+                        (const LdsD*)s_qs, s_rt, s_rp, s_ro, it & 3);
         RT_DBG_TEND(2, t_p);
         RT_DBG_TSTART(t_w2);
         __syncthreads();
@@ -375,6 +408,257 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
     RT_DBG_TFLUSH();
 }
 
+// Query-pool variant (RT_MK_FPOOL, default): the same per-vertex work as k_megakernel_flat_f64 but
+// without barriers. Each wave loops on its own: (1) for each mesh, if at least `pool_min` queries of
+// that mesh are queued in the block's LDS queue (or < 16 of the wave's paths are ready), it takes up to 64 of
+// them (any wave's, closest-hit and shadow mixed) and evaluates them with flat_query, one lane per
+// query; (2) each of its paths whose queries are all answered (s_pend = 0) adds the previous shadow
+// result, merges the mesh hits, shades, queues the shadow queries, and traces its next ray, queueing
+// that ray's closest-hit queries. A path thus waits only for its own queries, queries are evaluated
+// in fuller chunks, and no wave waits at a barrier for another wave's chunk (the block-synchronous
+// kernel spent 24% of its wave time in barrier waits, 2 waves of 4 working in phase P).
+constexpr int kFpRing = 512;  // per mesh: at most 256 closest-hit + 256 shadow queries queued at once
+
+template <int F, int W>
+__global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
+                                                                 uint32_t* next_sub, long nsub, int pool_min) {
+    using C = Cfg<F>;
+    static_assert(C::mesh && C::compact && !C::bvh, "flat-mesh kernel: compact scenes, octree meshes");
+    DevScene sc = sc_g;
+    __shared__ DevObject s_objs[kMaxCompactObjects];
+    {
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(sc_g.objects);
+        uint64_t* dst = reinterpret_cast<uint64_t*>(s_objs);
+        const int nw = sc_g.n_objects * (int)(sizeof(DevObject) / 8);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+        sc.objects = s_objs;
+    }
+    // per lane (one column per thread): subpixel accumulator; the closest-hit query ray (o, d), the
+    // shadow query ray (o, d, |y - x|); results per (mesh, lane); queries outstanding per lane
+    __shared__ double s_acc[3 * kBlk];
+    __shared__ double s_qc[6 * kBlk], s_qs[7 * kBlk];
+    __shared__ double s_rt[kFlatMeshes * kBlk];
+    __shared__ int32_t s_rp[kFlatMeshes * kBlk];
+    __shared__ uint8_t s_ro[kFlatMeshes * kBlk];
+    __shared__ int32_t s_pend[kBlk];
+    // per mesh: queued queries, entry = lane (closest hit) or 256 + lane (shadow)
+    __shared__ int32_t s_ring[kFlatMeshes][kFpRing];
+    __shared__ uint32_t s_head[kFlatMeshes], s_tail[kFlatMeshes];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kFlatMeshes * kFpRing; i += kBlk) (&s_ring[0][0])[i] = -1;
+    if (tid < kFlatMeshes) {
+        s_head[tid] = 0;
+        s_tail[tid] = 0;
+    }
+    s_pend[tid] = 0;
+    RT_DBG_TINIT();
+    __syncthreads();
+    LdsD* acc_l = (LdsD*)s_acc + tid;
+    const int nm = sc.n_meshes;
+
+    uint32_t nverts = 0;
+    const long n_split = nsub - a.n_whole;
+    const long nunits = a.n_wunits + n_split * a.tail_cps;
+    int id, end, s;
+    const long t0 = wave_ticket(next_sub, true);
+    unit_of(a, t0, id, end, s);
+    bool active = t0 < nunits;
+    acc_l[0] = 0.0; acc_l[kBlk] = 0.0; acc_l[2 * kBlk] = 0.0;
+    PathState ps;
+    bool fresh = true;
+    bool traced = false;   // ps.ray has been traced: h is its analytic hit, qmask its closest-hit queries
+    bool spend = false;    // a shadow query set of the last vertex is in flight (its NEE term in pc)
+    bool endwait = false;  // the path has ended; the sample is finished once the shadow result is in
+    HitRec h{0.0, -1, -1};
+    uint32_t qmask = 0, smask = 0;
+    V3 pc = v3(0, 0, 0);
+    while (__any(active)) {
+        RT_DBG_WAVE(8, lane_id_is0());
+        RT_DBG_TSTART(t_q);
+        // ---------------- (1) queued mesh queries, a chunk per mesh
+        {
+            const bool rdy = active && __hip_atomic_load(&s_pend[tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
+            // full chunks while this wave has paths to go on with; anything queued once most of its
+            // paths wait (also the frame's end: no query waits for a quorum that never comes)
+            const int need = __popcll(__ballot(rdy)) >= 16 ? pool_min : 1;
+            for (int m = 0; m < nm; ++m) {
+                const LdsQueue Q{s_ring[m], &s_head[m], &s_tail[m], (uint32_t)kFpRing - 1u};
+                const int32_t e = queue_take(Q, need);
+                if (!__any(e >= 0)) continue;
+                RT_DBG_WAVE(13, lane_id_is0());
+                RT_DBG_WAVE(12, e >= 0);
+                if (e >= 0) {
+                    const int kind = e >> 8, who = e & (kBlk - 1);
+                    const LdsD* q = kind ? (const LdsD*)s_qs : (const LdsD*)s_qc;
+                    const Ray r{v3(q[who], q[kBlk + who], q[2 * kBlk + who]),
+                                v3(q[3 * kBlk + who], q[4 * kBlk + who], q[5 * kBlk + who])};
+                    const RayInv inv = make_inv(r.d);
+                    double t = 0.0;
+                    int prim = -1;
+                    const bool hit = flat_query(sc, sc.meshes[m], r, inv, &t, &prim);
+                    if (kind == 0) {
+                        s_rt[m * kBlk + who] = t;
+                        s_rp[m * kBlk + who] = hit ? prim : -1;
+                    } else {
+                        s_ro[m * kBlk + who] = hit && !(t + 0.001 >= q[6 * kBlk + who]) ? 1 : 0;
+                    }
+                    __hip_atomic_fetch_sub(&s_pend[who], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+        }
+        RT_DBG_TEND(1, t_q);
+        RT_DBG_TSTART(t_v);
+        // ---------------- (2) paths whose queries are all answered
+        const bool ready = active && __hip_atomic_load(&s_pend[tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
+        RT_DBG_WAVE(9, ready);
+        bool finish = false, shadow_q = false;
+        Ray sr{v3(0, 0, 0), v3(0, 0, 1)};
+        double dist = 0.0;
+        if (ready) {
+            if (spend) {  // the last vertex's NEE term, unless a mesh blocks its shadow ray (mutually_visible)
+                bool occluded = false;
+                for (int m = 0; m < nm; ++m)
+                    if ((smask >> m) & 1u) occluded |= s_ro[m * kBlk + tid] != 0;
+                if (!occluded) ps.L = ps.L + pc;
+                spend = false;
+            }
+            if (endwait) {
+                endwait = false;
+                finish = true;
+            } else if (traced) {
+                CTab* T = tables(sc);
+                for (int g = 0; g < T->n_gen; ++g) {  // Scene::trace_ray's loop over the meshes (ties: lower index)
+                    const int idx = T->gen_idx[g];
+                    const DevObject& o = sc.objects[idx];
+                    if (o.geom == GEOM_MESH && ((qmask >> o.mesh) & 1u)) {
+                        const int p = s_rp[o.mesh * kBlk + tid];
+                        if (p >= 0) consider(h, s_rt[o.mesh * kBlk + tid], idx, p);
+                    }
+                }
+                nverts += h.obj >= 0;
+                ShadowDefer df;
+                df.pending = false;
+                const bool cont = shade_vertex<C>(sc, a, ps, h, &df);
+                traced = false;
+                if (df.pending) {  // the analytic objects let the shadow ray through; a mesh may block it
+                    shadow_q = true;
+                    pc = df.c;
+                    dist = df.dist;
+                    sr = Ray{df.o, df.d};
+                }
+                if (!cont) {
+                    if (shadow_q) endwait = true;
+                    else finish = true;
+                }
+            }
+        }
+        RT_DBG_TEND(2, t_v);
+        RT_DBG_TSTART(t_b);
+        // shadow queries of this vertex, per mesh near the segment
+        uint32_t want_s = 0;
+        if (shadow_q) {
+            const RayInv sinv = make_inv(sr.d);
+            for (int m = 0; m < nm; ++m) {
+                const DevMesh& M = sc.meshes[m];
+                if (near_box(M.cull_box, sr, sinv, M.cull_pad, dist)) want_s |= 1u << m;
+            }
+            if (want_s) {
+                s_qs[tid] = sr.o.x; s_qs[kBlk + tid] = sr.o.y; s_qs[2 * kBlk + tid] = sr.o.z;
+                s_qs[3 * kBlk + tid] = sr.d.x; s_qs[4 * kBlk + tid] = sr.d.y; s_qs[5 * kBlk + tid] = sr.d.z;
+                s_qs[6 * kBlk + tid] = dist;
+                spend = true;
+                smask = want_s;
+            } else {  // no mesh near the shadow segment: unblocked now
+                ps.L = ps.L + pc;
+                if (endwait) {
+                    endwait = false;
+                    finish = true;
+                }
+            }
+        }
+        // sample / subpixel bookkeeping, tickets
+        bool done = false;
+        if (finish) {
+            fresh = true;
+            if (id < a.n_whole) {
+                V3 acc = v3(acc_l[0], acc_l[kBlk], acc_l[2 * kBlk]);
+                acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                acc_l[0] = acc.x; acc_l[kBlk] = acc.y; acc_l[2 * kBlk] = acc.z;
+                if (++s == a.n_samples) {
+                    double* o = sub_buf + (size_t)id * 3;
+                    o[0] = acc.x;
+                    o[1] = acc.y;
+                    o[2] = acc.z;
+                    if (++id < end) {  // the next subpixel of the run, no ticket
+                        s = 0;
+                        acc_l[0] = 0.0; acc_l[kBlk] = 0.0; acc_l[2 * kBlk] = 0.0;
+                    } else {
+                        done = true;
+                    }
+                }
+            } else {  // split tail (k_tail_sum_f64)
+                double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
+                o[0] = ps.L.x;
+                o[1] = ps.L.y;
+                o[2] = ps.L.z;
+                done = !unit_has_next(a, id, s);
+                ++s;
+            }
+        }
+        bool stop = false;
+        if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+        const long nt = wave_ticket(next_sub, done && !stop);
+        if (__any(done)) flush_count(a.counters, nverts);
+        if (done) {
+            unit_of(a, nt, id, end, s);
+            active = !stop && nt < nunits;
+            acc_l[0] = 0.0; acc_l[kBlk] = 0.0; acc_l[2 * kBlk] = 0.0;
+            fresh = true;
+        }
+        // ---------------- the next ray (the path goes on, or a new sample), its closest-hit queries
+        const bool tr = ready && active && !endwait && !traced;
+        uint32_t want_c = 0;
+        if (tr) {
+            if (fresh) {
+                begin_sample(sc, a, subpixel_of(a, id), s, ps);
+                fresh = false;
+            }
+            const RayInv inv = make_inv(ps.ray.d);
+            h = trace_analytic<C>(sc, ps.ray, inv);
+            const double tmax = h.obj >= 0 ? h.t : INFINITY;
+            for (int m = 0; m < nm; ++m) {
+                const DevMesh& M = sc.meshes[m];
+                if (near_box(M.cull_box, ps.ray, inv, M.cull_pad, tmax)) want_c |= 1u << m;
+            }
+            if (want_c) {
+                s_qc[tid] = ps.ray.o.x; s_qc[kBlk + tid] = ps.ray.o.y; s_qc[2 * kBlk + tid] = ps.ray.o.z;
+                s_qc[3 * kBlk + tid] = ps.ray.d.x; s_qc[4 * kBlk + tid] = ps.ray.d.y; s_qc[5 * kBlk + tid] = ps.ray.d.z;
+            }
+            qmask = want_c;
+            traced = true;
+        }
+        // queue this lane's new queries (its s_pend is 0 until they are queued: nobody else writes it)
+        if (want_s | want_c) s_pend[tid] = __popc(want_s) + __popc(want_c);
+        for (int m = 0; m < nm; ++m) {
+            const LdsQueue Q{s_ring[m], &s_head[m], &s_tail[m], (uint32_t)kFpRing - 1u};
+            queue_put(Q, (want_s >> m) & 1u, kBlk + tid);
+            queue_put(Q, (want_c >> m) & 1u, tid);
+        }
+        RT_DBG_TEND(3, t_b);
+    }
+    flush_count(a.counters, nverts);
+    RT_DBG_TFLUSH();
+}
+
+template <int F, int W>
+static void launch_fpool(const DevScene& sc, RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
+                         double* tail_buf, size_t tail_cap, int pool_min, hipStream_t st) {
+    const long blocks = resident_blocks(k_megakernel_fpool_f64<F, W>, (nsub + kBlk - 1) / kBlk);
+    plan_tail(a, nsub, blocks * kBlk, tail_buf, tail_cap);
+    hipLaunchKernelGGL((k_megakernel_fpool_f64<F, W>), dim3((unsigned)blocks), dim3(kBlk), 0, st, sc, a, sub_buf,
+                       next_sub, nsub, pool_min);
+}
+
 template <int F, int W>
 static void launch_flat(const DevScene& sc, RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
                         double* tail_buf, size_t tail_cap, hipStream_t st) {
@@ -391,9 +675,14 @@ hipError_t launch_megakernel_flat_f64(const DevScene& sc, const RenderArgs& a_in
     const long nsub = (long)a_in.tw * a_in.th * 4;
     RenderArgs a = a_in;
     static const int waves = env_int("RT_MK_FLAT_WAVES", 3);
+    static const int fpool = env_int("RT_MK_FPOOL", 1);
+    static const int pool_min = env_int("RT_MK_FPOOL_MIN", 48);
 #define RT_FLAT_CASE(F)                                                                       \
     case F:                                                                                   \
-        if (waves == 2) launch_flat<F, 2>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, st); \
+        if (fpool) {                                                                          \
+            if (waves == 2) launch_fpool<F, 2>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, st); \
+            else launch_fpool<F, 3>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, st); \
+        } else if (waves == 2) launch_flat<F, 2>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, st); \
         else launch_flat<F, 3>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, st); \
         break;
     switch (a.features & 15) {
