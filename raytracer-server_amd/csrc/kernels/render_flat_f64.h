@@ -42,6 +42,46 @@ constexpr int kBlk = 256;
 typedef __attribute__((address_space(3))) double LdsD;
 typedef __attribute__((address_space(3))) uint64_t LdsU;
 
+// The first of the candidate octants `cand` (non-zero) in the walk's visiting order: the root's
+// octants sorted by (mag(centre - origin), index) (geometry.rs:1248-1260, a stable insertion sort;
+// root_order). Only the minimum is needed, so no sort: the argmin of the radicands d2 (sqrt is
+// monotone), unless a lower-index candidate's d2 lies within 2^-50 of the minimum, where the two
+// square roots may round equal and the index decides (then the argmin of the roots themselves).
+RT_DEV int first_visited(const DevMesh& m, const Ray& ray, uint32_t cand) {
+    double d2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const V3 dv = ld3(m.oct_center[i]) - ray.o;
+        d2[i] = dv.x * dv.x + dv.y * dv.y + dv.z * dv.z;  // mag()'s radicand, same order
+    }
+    int best = -1;
+    double bk = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if (((cand >> i) & 1u) && (best < 0 || d2[i] < bk)) {
+            best = i;
+            bk = d2[i];
+        }
+    }
+    bool close = false;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) close |= ((cand >> i) & 1u) && i < best && !(d2[i] > bk * (1.0 + 0x1p-50));
+    if (close) {  // rare: compare the roots (mag() itself), ties to the lower index
+        best = -1;
+        bk = 0.0;
+        for (int i = 0; i < 8; ++i) {
+            if ((cand >> i) & 1u) {
+                const double k = sqrt(d2[i]);
+                if (best < 0 || k < bk) {
+                    best = i;
+                    bk = k;
+                }
+            }
+        }
+    }
+    return best;
+}
+
 // Mesh::intersect of a flat octree for the ray (geometry.rs:883-905, 1237-1295): the walk visits the
 // root's children (leaves) in the ray's order (distances to the ROOT octant centres, root_order),
 // takes the first one whose octant box the ray hits (box_hit) and that holds a triangle hit, and
@@ -81,20 +121,7 @@ RT_DEV bool flat_query(const DevScene& sc, const DevMesh& m, const Ray& ray, con
         if (hit_leaves != 0) {
             uint32_t cand = hit_leaves & (uint32_t)m.flat_kids;
             cand &= octant_mask(m.root_box, m.root_box + 3, ray, inv);  // the children's box_hit, bit i = octant i
-            if (cand) {
-                double d2[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const V3 dv = ld3(m.oct_center[i]) - ray.o;
-                    d2[i] = dv.x * dv.x + dv.y * dv.y + dv.z * dv.z;  // mag()'s radicand, same order
-                }
-                const uint32_t order = root_order(d2);
-#pragma unroll
-                for (int q = 7; q >= 0; --q) {  // the first candidate in visiting order
-                    const int oi = (int)((order >> (4 * q)) & 0xFu);
-                    if ((cand >> oi) & 1u) win = oi;
-                }
-            }
+            if (cand) win = first_visited(m, ray, cand);
         }
     }
     if (win < 0) return false;
