@@ -431,6 +431,50 @@ struct WalkPool {
 enum : uint8_t { POOL_CLOSEST = 0, POOL_SHADOW = 1, POOL_DONE = 2 };
 constexpr int kPoolRefill = 8;  // refill only when at least this many lanes of the round are idle
 
+// Compact park of the walk pool (fits 3 blocks of 256 threads per CU, i.e. 3 waves/SIMD): no 1/d
+// (recomputed by make_inv when a query is loaded: the same bits), no NEE term (the owner keeps it in
+// registers), depth / pm / stk8 packed in one word. Doubles: ray o, d; box mn, mx; walk best t;
+// query t (closest hit so far / shadow distance). Ints: cur, depth | pm << 8 | stk8 << 16, path,
+// stk (2 words), order, lpos, lend, best, hit object, hit prim, gen slot, mesh, occluded.
+constexpr int kPark2D = 14, kPark2I = 14;
+enum : int { P2_T = 13, P2_HOBJ = 9, P2_HPRIM = 10, P2_OCC = 13 };
+RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
+    p.D(0) = r.wr.o.x; p.D(1) = r.wr.o.y; p.D(2) = r.wr.o.z;
+    p.D(3) = r.wr.d.x; p.D(4) = r.wr.d.y; p.D(5) = r.wr.d.z;
+    for (int k = 0; k < 3; ++k) { p.D(6 + k) = r.w.mn[k]; p.D(9 + k) = r.w.mx[k]; }
+    p.D(12) = r.w.bt;
+    p.D(13) = r.wt;
+    p.I(0) = r.w.cur;
+    p.I(1) = (int32_t)((uint32_t)r.w.depth | (r.w.pm << 8) | (r.w.stk8 << 16));
+    p.I(2) = (int32_t)r.w.path;
+    p.I(3) = (int32_t)(uint32_t)r.w.stk; p.I(4) = (int32_t)(uint32_t)(r.w.stk >> 32);
+    p.I(5) = (int32_t)r.w.order; p.I(6) = r.w.lpos; p.I(7) = r.w.lend; p.I(8) = r.w.best;
+    p.I(9) = r.hobj; p.I(10) = r.hprim; p.I(11) = r.g; p.I(12) = r.mi; p.I(13) = r.occluded;
+}
+RT_DEV void park2_load(const Park& p, WalkRegs& r) {
+    r.wr.o = v3(p.D(0), p.D(1), p.D(2));
+    r.wr.d = v3(p.D(3), p.D(4), p.D(5));
+    r.wi = make_inv(r.wr.d);
+    for (int k = 0; k < 3; ++k) { r.w.mn[k] = p.D(6 + k); r.w.mx[k] = p.D(9 + k); }
+    r.w.bt = p.D(12);
+    r.wt = p.D(13);
+    r.w.cur = p.I(0);
+    const uint32_t dps = (uint32_t)p.I(1);
+    r.w.depth = (int32_t)(dps & 0xFFu); r.w.pm = (dps >> 8) & 0xFFu; r.w.stk8 = dps >> 16;
+    r.w.path = (uint32_t)p.I(2);
+    r.w.stk = (uint64_t)(uint32_t)p.I(3) | ((uint64_t)(uint32_t)p.I(4) << 32);
+    r.w.order = (uint32_t)p.I(5); r.w.lpos = p.I(6); r.w.lend = p.I(7); r.w.best = p.I(8);
+    r.hobj = p.I(9); r.hprim = p.I(10); r.g = p.I(11); r.mi = p.I(12); r.occluded = p.I(13);
+}
+// A new pool query (see park_query).
+RT_DEV void park2_query(const Park& p, const Ray& r, double wt, int32_t hobj, int32_t hprim) {
+    p.D(0) = r.o.x; p.D(1) = r.o.y; p.D(2) = r.o.z;
+    p.D(3) = r.d.x; p.D(4) = r.d.y; p.D(5) = r.d.z;
+    p.D(13) = wt;
+    p.I(0) = -1;
+    p.I(9) = hobj; p.I(10) = hprim; p.I(11) = -1; p.I(13) = 0;
+}
+
 // One pool round: up to ksteps walk steps over queries taken from the pool; a lane whose query
 // finishes hands the result to its owner and, while steps remain, takes the next queued query
 // (refill: the round keeps its lanes full). Unfinished queries go back to the pool. All lanes call.
@@ -443,7 +487,7 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
     bool closest = false;
     auto col = [&](int32_t c) { return Park{park_d + c, park_i + c}; };
     if (q >= 0) {
-        park_load(col(q), r);
+        park2_load(col(q), r);
         closest = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == POOL_CLOSEST;
     }
     for (int k = 0; k < ksteps; ++k) {
@@ -476,10 +520,10 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
             }
             if (fin) {  // results for the owner's vertex phase, then the status word
                 const Park pq = col(q);
-                pq.D(16) = r.wt;
-                pq.I(11) = r.hobj;
-                pq.I(12) = r.hprim;
-                pq.I(15) = r.occluded;
+                pq.D(P2_T) = r.wt;
+                pq.I(P2_HOBJ) = r.hobj;
+                pq.I(P2_HPRIM) = r.hprim;
+                pq.I(P2_OCC) = r.occluded;
                 __hip_atomic_store(&wp.status[q], (uint8_t)POOL_DONE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 q = -1;
             }
@@ -488,12 +532,12 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
             const int32_t q2 = queue_take_each(wp.q, q < 0);
             if (q2 >= 0) {
                 q = q2;
-                park_load(col(q), r);
+                park2_load(col(q), r);
                 closest = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == POOL_CLOSEST;
             }
         }
     }
-    if (q >= 0) park_store(col(q), r);
+    if (q >= 0) park2_store(col(q), r);
     queue_put(wp.q, q >= 0, q);
     return true;
 }
@@ -517,8 +561,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
         sc.objects = s_objs;
     }
 #endif
-    __shared__ double s_park_d[kParkD * kParkThreads];
-    __shared__ int32_t s_park_i[kParkI * kParkThreads];
+    __shared__ double s_park_d[(P ? kPark2D : kParkD) * kParkThreads];
+    __shared__ int32_t s_park_i[(P ? kPark2I : kParkI) * kParkThreads];
     const Park park{(LdsDouble*)s_park_d + threadIdx.x, (LdsInt*)s_park_i + threadIdx.x};
     __shared__ int32_t s_ring[P ? 256 : 1];
     __shared__ uint8_t s_status[P ? 256 : 1];
@@ -530,11 +574,14 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
         __syncthreads();
     }
     // subpixel accumulator and camera-sample buffer in LDS, as in k_megakernel_f64
-    __shared__ double s_acc[3 * 256], s_nbd[3 * 256];
-    __shared__ uint64_t s_nbr[2 * 256];
+    // (no camera-sample buffer in pool mode: its 10 KB of LDS are what a third block per CU needs)
+    __shared__ double s_acc[3 * 256], s_nbd[P ? 1 : 3 * 256];
+    __shared__ uint64_t s_nbr[P ? 1 : 2 * 256];
     LdsDouble* acc_l = (LdsDouble*)s_acc + threadIdx.x;
-    LdsDouble* nbd = (LdsDouble*)s_nbd + threadIdx.x;
-    LdsU64* nbr = (LdsU64*)s_nbr + threadIdx.x;
+    LdsDouble* nbd = (LdsDouble*)s_nbd + (P ? 0 : threadIdx.x);
+    LdsU64* nbr = (LdsU64*)s_nbr + (P ? 0 : threadIdx.x);
+    if constexpr (P) refill = 0;
+    V3 pc = v3(0, 0, 0);  // pool: the pending shadow query's NEE term (the park has no room for it)
     uint32_t nverts = 0;
     // tickets: whole subpixels, then the split tail's chunks (unit_of), as in k_megakernel_f64
     const long n_split = nsub - a.n_whole;
@@ -578,18 +625,22 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
             bool shade_now = false, sample_end = false, trace_now = true;
             HitRec h;
             if (phase == PH_WALK_SHADOW) {  // the shadow result, then (path going on) the next trace
-                if (!park.I(15)) ps.L = ps.L + v3(park.D(17), park.D(18), park.D(19));
+                if constexpr (P) {
+                    if (!park.I(P2_OCC)) ps.L = ps.L + pc;
+                } else {
+                    if (!park.I(15)) ps.L = ps.L + v3(park.D(17), park.D(18), park.D(19));
+                }
                 phase = PH_TRACE;
                 sample_end = !cont;
                 trace_now = cont;
             } else if (phase == PH_WALK_CLOSEST) {
-                h = HitRec{park.D(16), park.I(11), park.I(12)};
+                h = P ? HitRec{park.D(P2_T), park.I(P2_HOBJ), park.I(P2_HPRIM)} : HitRec{park.D(16), park.I(11), park.I(12)};
                 shade_now = true;
                 trace_now = false;
             }
             if (trace_now) {
                 if (fresh) {
-                    if (nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[256], nbd[512]), nbr[0], nbr[256]}, ps);
+                    if (!P && nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[256], nbd[512]), nbr[0], nbr[256]}, ps);
                     else begin_sample(sc, a, subpixel_of(a, id), s, ps);
                     nvalid = false;
                     fresh = false;
@@ -597,7 +648,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                 const RayInv wi = make_inv(ps.ray.d);
                 h = trace_analytic<C>(sc, ps.ray, wi);
                 if (mesh_candidate<C>(sc, ps.ray, wi, h.obj >= 0 ? h.t : INFINITY)) {
-                    park_query(park, ps.ray, wi, h.t, h.obj, h.prim);
+                    if constexpr (P) park2_query(park, ps.ray, h.t, h.obj, h.prim);
+                    else park_query(park, ps.ray, wi, h.t, h.obj, h.prim);
                     if constexpr (P) s_status[threadIdx.x] = POOL_CLOSEST;
                     phase = PH_WALK_CLOSEST;
                     walking = true;
@@ -613,10 +665,15 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                 phase = PH_TRACE;
                 if (df.pending) {  // shade_vertex found a mesh that could block the shadow ray
                     const Ray sr{df.o, df.d};
-                    park_query(park, sr, make_inv(sr.d), df.dist, -1, -1);
-                    park.D(17) = df.c.x;
-                    park.D(18) = df.c.y;
-                    park.D(19) = df.c.z;
+                    if constexpr (P) {
+                        park2_query(park, sr, df.dist, -1, -1);
+                        pc = df.c;
+                    } else {
+                        park_query(park, sr, make_inv(sr.d), df.dist, -1, -1);
+                        park.D(17) = df.c.x;
+                        park.D(18) = df.c.y;
+                        park.D(19) = df.c.z;
+                    }
                     if constexpr (P) s_status[threadIdx.x] = POOL_SHADOW;
                     phase = PH_WALK_SHADOW;
                     walking = true;
@@ -799,14 +856,16 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, dou
     if (flat && a.all_flat && (a.features & 25) == 9)
         return launch_megakernel_flat_f64(sc, a, sub_buf, next_sub, tail_buf, tail_cap, refill, st);
     if (interleave && (a.features & 9) == 9 && a.mesh_nodes >= interleave && !((a.features & 16) && bvh_fused)) {
-        // octree walks through the block's walk pool (RT_MK_POOL=0: each lane walks its own query)
+        // octree walks through the block's walk pool, 2 waves/SIMD (RT_MK_POOL=3: 3 waves/SIMD, 37
+        // spilled VGPRs, measured 6% slower; 0: each lane walks its own query)
         static const int pool = env_int("RT_MK_POOL", 1);
         static const int pool_min = env_int("RT_MK_POOL_MIN", 32);
         static const int pool_ksteps = std::max(1, env_int("RT_MK_POOL_KSTEPS", 6));
         static const int pool_vmin = env_int("RT_MK_POOL_VMIN", 0);
 #define RT_MM_CASE(F)                                                                          \
     case F:                                                                                    \
-        if (pool) launch_mm<F, 2, true>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
+        if (pool == 3) launch_mm<F, 3, true>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
+        else if (pool) launch_mm<F, 2, true>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
         else launch_mm<F, 2, false>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, 0, 0, tail_buf, tail_cap, st); \
         break;
 #define RT_MMB_CASE(F)                                                                         \
