@@ -24,6 +24,12 @@
 #ifndef RT_OPT_VIS
 #define RT_OPT_VIS 1   // the shadow ray reuses norm(y - x) and |y - x| of the NEE term
 #endif
+#ifndef RT_OPT_LEF
+#define RT_OPT_LEF 1   // diffuse NEE: Le * f precomputed per object (DevObject::lef)
+#endif
+#ifndef RT_OPT_RR
+#define RT_OPT_RR 1    // Russian roulette as an integer comparison of the draw (Rng::below53)
+#endif
 
 namespace rt {
 namespace f64 {
@@ -175,7 +181,11 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
 #else
         const V3 i = norm(diff);
 #endif
-        V3 lef = mult(ld3(sc.objects[sc.light].emitted), brdf_eval<C>(obj, nrm, ps.o, i));
+        // Le * f: for a diffuse vertex Le_light * (kd / pi), evaluated once per object on the host
+        // (mirror vertices have no NEE)
+        V3 lef = (RT_OPT_LEF && (!C::phong || obj.brdf == BRDF_DIFFUSE))
+                     ? ld3(obj.lef)
+                     : mult(ld3(sc.objects[sc.light].emitted), brdf_eval<C>(obj, nrm, ps.o, i));
         if (!is_zero(lef)) {  // a zero Le*f makes the term exactly 0: skip the shadow ray
             RT_DBG_REGION(9);
             double vis;
@@ -220,7 +230,11 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
     }
     // Russian roulette (scene.rs:173 / :231) + BSDF continuation (scene.rs:176-184 / :232-240): one
     // code path for mirror and diffuse vertices
+#if RT_OPT_RR
+    if (!rng.below53(ps.depth <= (uint32_t)MAX_BOUNCES ? kP53One : kP53Survive)) return false;  // uniform() < p
+#else
     if (!(rng.uniform() < p)) return false;
+#endif
     RT_DBG_REGION(10);
     V3 wi;
     double pdf;

@@ -25,7 +25,8 @@ struct V3 {
     double x, y, z;
 };
 RT_DEV V3 v3(double x, double y, double z) { return V3{x, y, z}; }
-RT_DEV V3 ld3(const double* p) { return V3{p[0], p[1], p[2]}; }
+template <class P>
+RT_DEV V3 ld3(P p) { return V3{p[0], p[1], p[2]}; }  // any address space (scalar-loaded tables too)
 RT_DEV V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 RT_DEV V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 RT_DEV V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
@@ -231,8 +232,29 @@ struct Rng {
         s1 = rotl(b, 28);
         return r;
     }
-    RT_DEV double uniform() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
+#ifndef RT_OPT_UNIF
+#define RT_OPT_UNIF 0  // A/B: 1 = two 32-bit conversions and one FMA (same bits; measured 0.6% slower on
+                       // cornell_box, profiles/r02_ab.log r02z), 0 = the u64 -> f64 conversion
+#endif
+    // (u64 >> 11) * 2^-53, exactly: the 53-bit value is hi * 2^32 + lo (hi < 2^21); hi * 2^-21 and
+    // lo * 2^-53 are exact and so is their sum, so the FMA returns the exact product
+    RT_DEV double uniform() {
+#if RT_OPT_UNIF
+        const uint64_t v = next() >> 11;
+        return fma((double)(uint32_t)(v >> 32), 0x1p-21, (double)(uint32_t)v * 0x1p-53);
+#else
+        return (double)(next() >> 11) * (1.0 / 9007199254740992.0);
+#endif
+    }
+    // uniform() < p for p = thr * 2^-53 (thr an integer <= 2^53): the draw is v * 2^-53 exactly, so
+    // the comparison is v < thr, with no conversion (Russian roulette, scene.rs:173/:231)
+    RT_DEV bool below53(uint64_t thr) { return (next() >> 11) < thr; }
 };
+// Russian-roulette thresholds as 53-bit integers: p = 1 (depth <= MAX_BOUNCES) and p = 0.9, whose
+// double is M * 2^-53 for an integer M (0.9 lies in [0.5, 1))
+constexpr uint64_t kP53One = 1ull << 53;
+constexpr uint64_t kP53Survive = (uint64_t)(SURVIVAL_PROBABILITY * 9007199254740992.0);
+static_assert((double)kP53Survive == SURVIVAL_PROBABILITY * 9007199254740992.0, "0.9 * 2^53 must be an integer");
 
 // ---------------------------------------------------------------- primitives (geometry.rs:512-571)
 RT_DEV bool sphere_t(const DevObject& o, const Ray& ray, double* tout) {
@@ -268,8 +290,10 @@ RT_DEV bool plane_t(const DevObject& o, const Ray& ray, const RayInv& inv, doubl
     if (t >= 0.) { *tout = t; return true; }
     return false;
 }
-// Triangle::intersect (geometry.rs:637-670) on the precomputed (a, ab, ac, n).
-RT_DEV bool tri_t(const DevTri& tr, const Ray& ray, double* tout) {
+// Triangle::intersect (geometry.rs:637-670) on the precomputed (a, ab, ac, n); TR = DevTri in any
+// address space (flat_query reads its triangles through a constant-address-space pointer: s_load).
+template <class TR>
+RT_DEV bool tri_t(const TR& tr, const Ray& ray, double* tout) {
     V3 n = ld3(tr.n);
     if (fabs(dot(n, ray.d)) < 0.0001) return false;
     V3 ab = ld3(tr.ab), ac = ld3(tr.ac);
@@ -500,10 +524,22 @@ struct OctWalk {
 
 // Mask `cur`'s existing children whose boxes the ray hits, permuted to visiting order. (The child
 // table itself is not kept in registers: a pick reads its one entry again, an L2 hit.)
-RT_DEV void walk_enter(const DevScene& sc, const Ray& ray, const RayInv& inv, OctWalk& w) {
+// `top`: the LDS copy of this mesh's top levels (scene_layout.h: top_slot), or null; a node at depth
+// <= kTopDepth is then read from it (ds_read) instead of node_kids.
+typedef __attribute__((address_space(3))) int32_t LdsTopI32;
+RT_DEV void walk_enter(const DevScene& sc, const Ray& ray, const RayInv& inv, OctWalk& w,
+                       const LdsTopI32* top = nullptr) {
     RT_DBG(2);
-    const int4* k4 = reinterpret_cast<const int4*>(sc.node_kids + 8 * (size_t)w.cur);
-    const int4 ka = k4[0], kb = k4[1];
+    int4 ka, kb;
+    if (top && w.depth <= kTopDepth) {
+        const LdsTopI32* t = top + 8 * top_slot(w.depth, w.path);
+        ka = int4{t[0], t[1], t[2], t[3]};
+        kb = int4{t[4], t[5], t[6], t[7]};
+    } else {
+        const int4* k4 = reinterpret_cast<const int4*>(sc.node_kids + 8 * (size_t)w.cur);
+        ka = k4[0];
+        kb = k4[1];
+    }
     const int32_t kid[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
     uint32_t m = octant_mask(w.mn, w.mx, ray, inv);
 #pragma unroll
@@ -517,7 +553,7 @@ RT_DEV void walk_enter(const DevScene& sc, const Ray& ray, const RayInv& inv, Oc
 // Starts a walk; false if the ray cannot produce a usable hit on this mesh (empty mesh, or the
 // conservative near_box cull). tmax: see near_box.
 RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax,
-                       OctWalk& w) {
+                       OctWalk& w, const LdsTopI32* top = nullptr) {
     if (m.n_nodes == 0) return false;
     RT_DBG(0);
     if (!near_box(m.cull_box, ray, inv, m.cull_pad, tmax)) return false;
@@ -550,7 +586,7 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
         w.mn[k] = m.root_box[k];
         w.mx[k] = m.root_box[3 + k];
     }
-    walk_enter(sc, ray, inv, w);
+    walk_enter(sc, ray, inv, w, top);
     return true;
 }
 
@@ -597,7 +633,7 @@ RT_DEV int leaf_tris(const DevScene& sc, const Ray& ray, OctWalk& w, double* t, 
     return -1;
 }
 RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w, double* t,
-                     int* prim) {
+                     int* prim, const LdsTopI32* top = nullptr) {
     RT_DBG(5);
     if (w.lpos < w.lend) {  // triangles of the open leaf
         const int st = leaf_tris(sc, ray, w, t, prim);
@@ -605,15 +641,20 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
     }
     if (w.pm == 0) {  // `cur` exhausted: resume at the nearest ancestor with children left
         int lv = w.depth;
-        int32_t cur = w.cur;
         uint32_t pm = 0;
         while (pm == 0 && lv > 0) {
-            cur = sc.node_up[cur].x;
             --lv;
             pm = lv < 8 ? (uint32_t)(w.stk >> (8 * lv)) & 0xFFu : w.stk8;
         }
         if (pm == 0) return WALK_MISS;  // the root is exhausted
-        w.cur = cur;
+        // the ancestor's node id through the parent links; not needed (and not loaded) when its
+        // level is read from the LDS top levels (w.cur then keeps a stale id >= 0 until the next
+        // descent sets it from a child entry)
+        if (!(top && lv <= kTopDepth)) {
+            int32_t cur = w.cur;
+            for (int l = w.depth; l > lv; --l) cur = sc.node_up[cur].x;
+            w.cur = cur;
+        }
         w.depth = lv;
         w.pm = pm;
         w.path &= (1u << (3 * lv)) - 1u;
@@ -635,7 +676,8 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
     const int q = __builtin_ctz(w.pm);
     w.pm &= w.pm - 1u;
     const uint32_t oi = (w.order >> (4 * q)) & 0xF;
-    const int32_t c = sc.node_kids[8 * (size_t)w.cur + oi];
+    const int32_t c = (top && w.depth <= kTopDepth) ? top[8 * top_slot(w.depth, w.path) + (int)oi]
+                                                    : sc.node_kids[8 * (size_t)w.cur + oi];
     if (c <= -2) {  // open a leaf
         RT_DBG(3);
         const int32_t e = -2 - c;  // the leaf's range inline (kid_leaf), or its id behind the escape count
@@ -667,7 +709,7 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         const double cc = (w.mn[k] + w.mx[k]) / 2.0;
         if ((oi >> (2 - k)) & 1u) w.mn[k] = cc; else w.mx[k] = cc;
     }
-    walk_enter(sc, ray, inv, w);
+    walk_enter(sc, ray, inv, w, top);
     return WALK_RUN;
 }
 
@@ -1068,7 +1110,10 @@ RT_DEV bool mesh_occludes(const DevScene& sc, const Ray& r, const RayInv& inv, d
 // ---------------------------------------------------------------- BRDF (scene.rs:30-123)
 template <class C>
 RT_DEV V3 brdf_eval(const DevObject& o, V3 n, V3 out, V3 in) {
-    if (o.brdf == BRDF_DIFFUSE) return ld3(o.k) * FRAC_1_PI;
+#ifndef RT_OPT_KPI
+#define RT_OPT_KPI 1  // A/B: diffuse f = kd * FRAC_1_PI read from the object (host-evaluated, same bits)
+#endif
+    if (o.brdf == BRDF_DIFFUSE) return RT_OPT_KPI ? ld3(o.kpi) : ld3(o.k) * FRAC_1_PI;
     if (!C::phong || o.brdf == BRDF_SPECULAR) {
         if (equal_within(in, flip_across(out, n), 0.001)) return ld3(o.k) / dot(n, in);
         return v3(0, 0, 0);
@@ -1173,8 +1218,9 @@ RT_DEV Ray camera_ray(const DevScene& sc, V3 cx, V3 cy, double w, double h, int 
     double dx = r1 < 1. ? sqrt(r1) - 1. : 1. - sqrt(2. - r1);
     double r2 = 2. * u2;
     double dy = r2 < 1. ? sqrt(r2) - 1. : 1. - sqrt(2. - r2);
-    V3 d = cx * ((((double)sx + 0.5 + dx) / 2. + (double)x) / w - 0.5) +
-           cy * ((((double)sy + 0.5 + dy) / 2. + (double)y) / h - 0.5) + ld3(sc.cam_dir);
+    // w, h are image sizes in [1, 2^32]: the shared-divisor division is exact (qdiv)
+    V3 d = cx * (qdiv(((double)sx + 0.5 + dx) / 2. + (double)x, w, rcp_rn(w)) - 0.5) +
+           cy * (qdiv(((double)sy + 0.5 + dy) / 2. + (double)y, h, rcp_rn(h)) - 0.5) + ld3(sc.cam_dir);
     return Ray{ld3(sc.cam_pos), norm(d)};
 }
 

@@ -30,6 +30,8 @@ struct alignas(16) DevObject {
     int32_t emissive;     // emitted != 0 (any component)
     int32_t axis;         // plane with n == +-e_axis exactly (0,1,2), else -1
     int32_t pad0, pad1;
+    double kpi[3];        // diffuse: kd * FRAC_1_PI (Diffuse::eval, scene.rs:41-43), host-evaluated
+    double lef[3];        // diffuse: light's emitted * kpi (the NEE term's Le * f), host-evaluated
 };
 
 // Octree of one mesh, flattened in the reference's DFS pre-order (geometry.rs:1164-1216) so node
@@ -49,7 +51,10 @@ struct alignas(16) DevMesh {
     double surface_area;      // Mesh.surface_area (mesh-light pdf, geometry.rs:591)
     double total_weight;      // sum of triangle areas (WeightedIndex total)
     double cull_pad;          // near_box padding: 1e-7 * max(1, |box coordinates|)
-    int32_t btri_base, pad0, pad1, pad2;  // first of this mesh's n_tris BVH-order triangles (DevScene::btris)
+    int32_t btri_base;        // first of this mesh's n_tris BVH-order triangles (DevScene::btris)
+    int32_t top_base;         // this mesh's top-levels child table in DevScene::top_kids (kTopNodes x 8
+                              // entries), or -1 (root leaf / empty octree)
+    int32_t pad1, pad2;
     // Flat octree (the cubes): the root is a leaf, or a parent whose children are all leaves, with at
     // most kFlatMaxTris triangles and every leaf list in triangle order. flat_leaf[j / 4] byte j % 4 =
     // the leaves (octant bits; bit 0 for a root leaf) that hold triangle j; flat_kids = octants with a
@@ -77,6 +82,16 @@ constexpr int32_t kKidCountEscape = 63;
 RT_LAYOUT_FN int32_t kid_leaf(int32_t leaf, int32_t first, int32_t count) {
     const bool inl = count < kKidCountEscape && first < (1 << 25);
     return -2 - ((inl ? first : leaf) << 6 | (inl ? count : kKidCountEscape));
+}
+// Top levels of an octree (depths 0..kTopDepth), indexed by position instead of node id, so a walk
+// can read them from an LDS copy without knowing the node id: the node at depth d reached through
+// octant slots o_0, o_1, .., o_{d-1} (the walk's `path`, 3 bits per level, level 0 lowest) is entry
+// top_slot(d, path); its 8 child entries are the node_kids values (kKidEmpty where no node exists).
+constexpr int kTopDepth = 3;
+constexpr int kTopNodes = 1 + 8 + 64 + 512;  // 585 nodes x 32 B = 18.3 KB
+RT_LAYOUT_FN int top_slot(int depth, uint32_t path) {
+    const int off = depth == 0 ? 0 : depth == 1 ? 1 : depth == 2 ? 9 : 73;  // (8^d - 1) / 7
+    return off + (int)(path & ((1u << (3 * depth)) - 1u));
 }
 // node_up[node] = {parent node (-1 at the root), octant slot in the parent}
 // leaf_span[leaf] = {first entry of the leaf in ltri_id (ltris in RT_LTRI_INDEX=0 builds), count}
@@ -159,6 +174,9 @@ struct DevScene {
     const Bvh32* bvh32;
     const Tri32* btris32;
     const Compact32* ctab32;    // f32 compact tables (ok == 0: the generic object loop)
+    const int32_t* top_kids;    // top-levels child tables of the meshes (DevMesh::top_base)
+    int32_t top_mesh;           // the mesh whose top levels the walk-pool kernel stages in LDS, -1 none
+    int32_t top_pad;
     float off32;                // f32 mode: hit points are offset by off32 * n (scene-scaled epsilon)
     int32_t n_objects, light, n_meshes, compact;
     double cam_pos[3], cam_dir[3];

@@ -186,12 +186,14 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
 
 // Begins the octree walk of the next candidate mesh after gen slot g (Scene::trace_ray's /
 // mutually_visible's loop over the mesh objects); false when no mesh is left.
+// `top`: the LDS copy of mesh sc.top_mesh's top levels (walk-pool kernel), or null.
 template <class C>
 RT_DEV bool next_mesh_walk(const DevScene& sc, const Ray& r, const RayInv& inv, double tmax, int& g, int& mi,
-                           OctWalk& w) {
+                           OctWalk& w, const LdsTopI32* top = nullptr) {
     for (++g; g < tables(sc)->n_gen; ++g) {
         const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
-        if (o.geom == GEOM_MESH && walk_begin(sc, sc.meshes[o.mesh], r, inv, tmax, w)) {
+        if (o.geom == GEOM_MESH &&
+            walk_begin(sc, sc.meshes[o.mesh], r, inv, tmax, w, o.mesh == sc.top_mesh ? top : nullptr)) {
             mi = o.mesh;
             return true;
         }
@@ -480,7 +482,7 @@ RT_DEV void park2_query(const Park& p, const Ray& r, double wt, int32_t hobj, in
 // (refill: the round keeps its lanes full). Unfinished queries go back to the pool. All lanes call.
 template <class C>
 RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d, LdsInt* park_i, int need,
-                       int ksteps) {
+                       int ksteps, const LdsTopI32* top) {
     int32_t q = queue_take(wp.q, need);
     if (!__any(q >= 0)) return false;
     WalkRegs r;
@@ -497,11 +499,11 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
             bool fin = false;
             if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
                 const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
-                fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w);
+                fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, top);
             } else {
                 double t;
                 int prim;
-                const int st = walk_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim);
+                const int st = walk_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim, r.mi == sc.top_mesh ? top : nullptr);
                 if (st != WALK_RUN) {
                     if (closest) {
                         if (st == WALK_HIT) {
@@ -568,9 +570,18 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     __shared__ uint8_t s_status[P ? 256 : 1];
     __shared__ uint32_t s_qhead, s_qtail;
     const WalkPool wp{LdsQueue{s_ring, &s_qhead, &s_qtail, 255u}, s_status};
+    // pool: the top kTopDepth + 1 levels of the deepest mesh's octree in LDS (18.3 KB; the walks of
+    // every query of the block start there), scene_layout.h: top_slot
+    __shared__ int4 s_top[P ? kTopNodes * 2 : 1];
+    const LdsTopI32* top = nullptr;
     if constexpr (P) {
         s_ring[threadIdx.x] = -1;
         if (threadIdx.x == 0) { s_qhead = 0; s_qtail = 0; }
+        if (sc.top_mesh >= 0) {
+            const int4* src = reinterpret_cast<const int4*>(sc.top_kids + sc.meshes[sc.top_mesh].top_base);
+            for (int i = threadIdx.x; i < kTopNodes * 2; i += blockDim.x) s_top[i] = src[i];
+            top = (const LdsTopI32*)(LdsInt*)s_top;
+        }
         __syncthreads();
     }
     // subpixel accumulator and camera-sample buffer in LDS, as in k_megakernel_f64
@@ -605,7 +616,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
         if constexpr (P) {
             // take queued queries (at least pool_min of them while this wave has paths to shade)
             const int ready = __popcll(__ballot(active && !walking));
-            took = pool_round<C>(sc, wp, (LdsDouble*)s_park_d, (LdsInt*)s_park_i, ready ? pool_min : 1, ksteps);
+            took = pool_round<C>(sc, wp, (LdsDouble*)s_park_d, (LdsInt*)s_park_i, ready ? pool_min : 1, ksteps, top);
             if (!took && !ready) {
                 __builtin_amdgcn_s_sleep(2);  // every path of this wave waits on walks other waves hold
             }

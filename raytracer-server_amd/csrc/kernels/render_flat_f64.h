@@ -47,7 +47,8 @@ typedef __attribute__((address_space(3))) uint64_t LdsU;
 // root_order). Only the minimum is needed, so no sort: the argmin of the radicands d2 (sqrt is
 // monotone), unless a lower-index candidate's d2 lies within 2^-50 of the minimum, where the two
 // square roots may round equal and the index decides (then the argmin of the roots themselves).
-RT_DEV int first_visited(const DevMesh& m, const Ray& ray, uint32_t cand) {
+template <class MT>
+RT_DEV int first_visited(const MT& m, const Ray& ray, uint32_t cand) {
     double d2[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -89,8 +90,9 @@ RT_DEV int first_visited(const DevMesh& m, const Ray& ray, uint32_t cand) {
 // Evaluated here from every triangle's tri_t (the walk's own test, same bits) with the nearest hit
 // kept per leaf; box tests and the order only for lanes with a hit. A root leaf is its nearest hit
 // without any box test (geometry.rs:1237-1241). All lanes of the calling wave query mesh `m`.
-RT_DEV bool flat_query(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double* t_out,
-                       int* prim_out) {
+// (The general form, for rays with 3 or more triangle hits: flat_query below.)
+RT_DEV bool flat_query_leaves(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double* t_out,
+                              int* prim_out) {
     double bt[8];
     int bi[8];
 #pragma unroll
@@ -139,6 +141,66 @@ RT_DEV bool flat_query(const DevScene& sc, const DevMesh& m, const Ray& ray, con
     return true;
 }
 
+// The mesh and triangle tables of a flat query through constant-address-space pointers: every lane
+// of the wave queries the same mesh, so the triangle loop reads them with scalar loads into SGPRs
+// (no vector-memory round trip per triangle, no VGPRs for the 96 B of each triangle).
+typedef const __attribute__((address_space(4))) DevMesh CMesh;
+typedef const __attribute__((address_space(4))) DevTri CTri;
+
+// flat_query_leaves' result from the first two triangle hits of the ray (a ray crosses a convex
+// mesh's surface twice; a third hit, e.g. on an edge two triangles share, takes flat_query_leaves):
+// the winning leaf is found as there, from the union of the hit triangles' leaves, and its nearest
+// hit is the first of the two hits that lies in it unless the second is strictly nearer (the leaf
+// lists are in triangle order, so the earlier hit is the lower index: the walk's strict <). Same
+// bits as flat_query_leaves, without its per-leaf best-hit updates (8 leaves x 4 VALU per triangle).
+RT_DEV bool flat_query(const DevScene& sc, int mi, const Ray& ray, const RayInv& inv, double* t_out, int* prim_out) {
+    CMesh* M = (CMesh*)(uintptr_t)(sc.meshes + mi);
+    const int n = M->n_tris, base = M->tri_base;
+    CTri* T = (CTri*)(uintptr_t)(sc.tris + base);
+    double ta = 0.0, tb = 0.0;
+    int ja = -1, jb = -1, nh = 0;
+    uint32_t la = 0, lb = 0, hit_leaves = 0;
+    for (int j = 0; j < n; ++j) {
+        double tt;
+        if (tri_t(T[j], ray, &tt)) {
+            const uint32_t lm = (M->flat_leaf[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            hit_leaves |= lm;
+            if (nh == 0) {
+                ta = tt;
+                ja = j;
+                la = lm;
+            } else if (nh == 1) {
+                tb = tt;
+                jb = j;
+                lb = lm;
+            }
+            ++nh;
+        }
+    }
+    if (__any(nh > 2)) {
+        if (nh > 2) return flat_query_leaves(sc, sc.meshes[mi], ray, inv, t_out, prim_out);
+    }
+    int win = -1;
+    if (M->flat_root_leaf) {
+        win = nh > 0 ? 0 : -1;
+    } else if (__any(hit_leaves != 0)) {
+        if (hit_leaves != 0) {
+            uint32_t cand = hit_leaves & (uint32_t)M->flat_kids;
+            double rb[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) rb[k] = M->root_box[k];
+            cand &= octant_mask(rb, rb + 3, ray, inv);  // the children's box_hit, bit i = octant i
+            if (cand) win = first_visited(*M, ray, cand);
+        }
+    }
+    if (win < 0) return false;
+    const bool ina = ((la >> win) & 1u) != 0, inb = nh > 1 && ((lb >> win) & 1u) != 0;
+    const bool use_b = inb && (!ina || tb < ta);
+    *t_out = use_b ? tb : ta;
+    *prim_out = base + (use_b ? jb : ja);
+    return true;
+}
+
 // Appends this block's lane `tid` to queue q (wave-aggregated LDS atomic). All lanes of the wave call.
 RT_DEV void enqueue(int32_t* cnt, int32_t* queue, bool want) {
     const unsigned long long mk = __ballot(want);
@@ -184,7 +246,7 @@ RT_DEV void process_queries(const DevScene& sc, const int32_t* cnt_c, const int3
                 const RayInv inv = make_inv(r.d);
                 double t = 0.0;
                 int prim = -1;
-                const bool hit = flat_query(sc, sc.meshes[m], r, inv, &t, &prim);
+                const bool hit = flat_query(sc, m, r, inv, &t, &prim);
                 if (kind == 0) {
                     rt[m * kBlk + who] = t;
                     rp[m * kBlk + who] = hit ? prim : -1;
@@ -213,7 +275,7 @@ RT_DEV void process_queries(const DevScene& sc, const int32_t* cnt_c, const int3
                     const RayInv inv = make_inv(r.d);
                     double t = 0.0;
                     int prim = -1;
-                    const bool hit = flat_query(sc, sc.meshes[m], r, inv, &t, &prim);
+                    const bool hit = flat_query(sc, m, r, inv, &t, &prim);
                     if (kind == 0) {
                         rt[m * kBlk + who] = t;
                         rp[m * kBlk + who] = hit ? prim : -1;
@@ -522,7 +584,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                     const RayInv inv = make_inv(r.d);
                     double t = 0.0;
                     int prim = -1;
-                    const bool hit = flat_query(sc, sc.meshes[m], r, inv, &t, &prim);
+                    const bool hit = flat_query(sc, m, r, inv, &t, &prim);
                     if (kind == 0) {
                         s_rt[m * kBlk + who] = t;
                         s_rp[m * kBlk + who] = hit ? prim : -1;

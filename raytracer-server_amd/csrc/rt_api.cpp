@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -56,6 +57,7 @@ struct Packed {
     std::vector<rt::DevBvhNode> bvh;  // nearest-triangle mode (RT_FLAG_MESH_NEAREST)
     std::vector<rt::DevTri> btris;
     std::vector<int32_t> btri_id;
+    std::vector<int32_t> top_kids;  // [mesh tables][kTopNodes][8]: octree top levels by position (top_slot)
 };
 
 struct DeviceCopy {
@@ -347,6 +349,22 @@ void pack_scene(rt_scene* s) {
                                                : c8 + dm.node_base);
             }
         }
+        // top levels (depths 0..kTopDepth) by position: what the walk-pool kernel stages in LDS
+        dm.top_base = -1;
+        if (oc.size() > 0 && !oc.kind[0]) {
+            dm.top_base = (int32_t)p.top_kids.size();
+            p.top_kids.resize(p.top_kids.size() + (size_t)rt::kTopNodes * 8, rt::kKidEmpty);
+            int32_t* top = p.top_kids.data() + dm.top_base;
+            std::function<void(int32_t, int, uint32_t)> fill = [&](int32_t node, int depth, uint32_t path) {
+                const int slot = rt::top_slot(depth, path);
+                for (int k = 0; k < 8; ++k) {
+                    const int32_t e = p.kids[8 * (size_t)node + k];
+                    top[8 * slot + k] = e;
+                    if (e >= 0 && depth < rt::kTopDepth) fill(e, depth + 1, path | (uint32_t)k << (3 * depth));
+                }
+            };
+            fill(dm.node_base, 0, 0u);
+        }
         p.meshes.push_back(dm);
     }
     for (const Object& o : sc.objects) {
@@ -374,6 +392,15 @@ void pack_scene(rt_scene* s) {
             if (nz == 1 && std::fabs(n3[ax]) == 1.0) d.axis = ax;
         }
         p.objects.push_back(d);
+    }
+    // diffuse objects: kd / pi and the NEE term's Le_light * kd / pi, with the device's operations
+    // (path_f64.h brdf_eval: ld3(k) * FRAC_1_PI; integrator_f64.h: mult(Le, f)), so the same bits
+    const double FRAC_1_PI = 0.318309886183790671537767526745028724;  // path_f64.h FRAC_1_PI
+    for (rt::DevObject& d : p.objects) {
+        if (d.brdf != rt::BRDF_DIFFUSE) continue;
+        for (int k = 0; k < 3; ++k) d.kpi[k] = d.k[k] * FRAC_1_PI;
+        if (sc.light >= 0 && sc.light < (int)p.objects.size())
+            for (int k = 0; k < 3; ++k) d.lef[k] = p.objects[sc.light].emitted[k] * d.kpi[k];
     }
 }
 
@@ -542,6 +569,8 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         put(blob, &o_obj32, obj32);
         put(blob, &o_bvh32, bvh32);
         put(blob, &o_tri32, tri32);
+        size_t o_top;
+        put(blob, &o_top, p.top_kids);
         void* d = nullptr;
         HIP_TRY(hipMalloc(&d, blob.size()));
         hipError_t e = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice);
@@ -571,6 +600,18 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.off32 = off32;
         ds.ctab32 = (const rt::Compact32*)(b + o_tab32);
         ds.compact = compact;
+        // the walk-pool kernel stages the top levels of the largest octree in LDS (RT_MK_TOP=0: off, A/B)
+        ds.top_kids = (const int32_t*)(b + o_top);
+        ds.top_mesh = -1;
+        const char* top_env = std::getenv("RT_MK_TOP");
+        if (!(top_env && std::atoi(top_env) == 0)) {
+            int32_t most = 0;
+            for (size_t i = 0; i < p.meshes.size(); ++i)
+                if (p.meshes[i].top_base >= 0 && p.meshes[i].n_nodes > most) {
+                    most = p.meshes[i].n_nodes;
+                    ds.top_mesh = (int32_t)i;
+                }
+        }
         ds.light = s->host.light;
         ds.light_pdf = 0.0;
         if (ds.light >= 0 && ds.light < (int32_t)p.objects.size()) {
