@@ -606,18 +606,34 @@ constexpr int kTrisPerStep = RT_TRIS_PER_STEP;
 #endif
 // Up to kTrisPerStep triangles of the open leaf: WALK_RUN (triangles left), WALK_HIT (the leaf is
 // done and has a hit: the first leaf with a hit wins, geometry.rs:1267-1269), or -1 (done, no hit).
+#ifndef RT_TRI_PRELOAD
+#define RT_TRI_PRELOAD 1  // A/B: the step's triangles are loaded whole before any test (1), or by tri_t (0)
+#endif
 RT_DEV int leaf_tris(const DevScene& sc, const Ray& ray, OctWalk& w, double* t, int* prim) {
+#if RT_TRI_PRELOAD && !RT_LTRI_INDEX
+    // All of the step's triangles (96 B each) are loaded up front: tri_t reads a triangle's normal,
+    // tests |n . d| and only then its other 72 B, and the next triangle only after that, i.e. four
+    // dependent trips to L2 / the Infinity Cache per step. Entries past the leaf's end are clamped
+    // to its last one (loaded, never tested).
+    DevTri tr[kTrisPerStep];
+#pragma unroll
+    for (int j = 0; j < kTrisPerStep; ++j) tr[j] = sc.ltris[max(0, min(w.lpos + j, w.lend - 1))];
+#endif
 #pragma unroll
     for (int j = 0; j < kTrisPerStep; ++j) {
         if (w.lpos < w.lend) {
             RT_DBG(4);
             double tt;
-#if RT_LTRI_INDEX
-            const DevTri& tr = sc.tris[sc.ltri_id[w.lpos]];  // leaf list = triangle indices (3.6 MB table)
+#if RT_TRI_PRELOAD && !RT_LTRI_INDEX
+            if (tri_t(tr[j], ray, &tt) && (w.best < 0 || tt < w.bt)) {
 #else
-            const DevTri& tr = sc.ltris[w.lpos];  // leaf list = triangle copies (18 MB for the unicorn)
+#if RT_LTRI_INDEX
+            const DevTri& trj = sc.tris[sc.ltri_id[w.lpos]];  // leaf list = triangle indices (3.6 MB table)
+#else
+            const DevTri& trj = sc.ltris[w.lpos];  // leaf list = triangle copies (18 MB for the unicorn)
 #endif
-            if (tri_t(tr, ray, &tt) && (w.best < 0 || tt < w.bt)) {
+            if (tri_t(trj, ray, &tt) && (w.best < 0 || tt < w.bt)) {
+#endif
                 w.bt = tt;
                 w.best = w.lpos;
             }

@@ -175,16 +175,25 @@ def test_spp_semantics(rt, gpu_scenes, oracle_scenes):
 
 
 def test_sample_pixel_and_chunks(rt, gpu_scenes, oracle_scenes):
+    """sample_pixel and RenderJob.run (the reference's per-pixel seam and chunk loop, server.rs:157-199,
+    320-368) against the CPU oracle's render of the same pixels, and against the full GPU frame."""
     s = gpu_scenes["cornell_box"]
     w, h, spp = 60, 45, 8
-    full, _, _ = rt.render(s, w, h, spp, SEED)
+    full, sub_full, _ = rt.render(s, w, h, spp, SEED, want_sub=True)
+    rgb_o, sub_o, _ = oracle_scenes["cornell_box"].render(w, h, spp, SEED)
+    _assert_parity(full, sub_full, rgb_o, sub_o, "60x45 frame")
     # sample_pixel takes the reference's bottom-up y
-    assert rt.sample_pixel(10, h - 1 - 7, w, h, spp, s, seed=SEED) == tuple(int(c) for c in full[7, 10])
+    px = rt.sample_pixel(10, h - 1 - 7, w, h, spp, s, seed=SEED)
+    assert px == tuple(int(c) for c in full[7, 10])
+    assert np.all(np.abs(np.array(px) - rgb_o[7, 10].astype(int)) <= 1)
     msgs = rt.RenderJob(seed=SEED).run(s, w, h, spp)
     assert len(msgs) == h  # 60 px per message, one message per row at w = 60
     m = msgs[3]
     assert m[0] == 0 and m[1] == 60 and m[2:4] == (0).to_bytes(2, "little") and m[4:6] == (3).to_bytes(2, "little")
     assert m[6:] == full[3].tobytes()
+    # every chunk against the oracle's frame (RGB8 within 1: the parity bound of _assert_parity)
+    got = np.frombuffer(b"".join(bytes(x[6:]) for x in msgs), dtype=np.uint8).reshape(h, w, 3)
+    assert np.abs(got.astype(int) - rgb_o.astype(int)).max() <= 1
 
 
 def test_full_frame_properties(rt, gpu_scenes, oracle_scenes):
