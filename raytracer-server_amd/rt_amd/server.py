@@ -173,6 +173,11 @@ def main(argv=None):
     port = int(os.environ.get("PORT", "8080"))  # main.rs:38
     print(f"Listening on port {port}.")
     fp32 = os.environ.get("RT_PRECISION", "f64") == "f32"  # f64 (the reference's arithmetic) by default
+    if fp32:
+        # the f32 mode traces meshes with the nearest-triangle semantics
+        # (geometry.rs:886-903), not the reference's first-hit octree walk (geometry.rs:1237-1295)
+        print("RT_PRECISION=f32: f32 perf mode; meshes (flying_unicorn) use nearest-triangle hits, not the "
+              "reference's octree semantics; frames differ statistically from server.rs", file=sys.stderr)
     web.run_app(Server(scenes, renderer=gpu_band_renderer(fp32=fp32)).app(), host="0.0.0.0", port=port, print=None)
     return 0
 

@@ -354,6 +354,33 @@ def test_extra_assets_parity(asset, rt, oracle, tmp_path):
     _assert_fp32_stats(sub_f, sub_d, rgb_f, rgb_d, f"{asset}/f32")
 
 
+def test_two_deep_meshes_parity(rt, oracle, tmp_path):
+    """Two deep octrees in one scene (chair.obj and crewmate.obj side by side): the walk-pool kernel
+    stages the larger octree's top levels in LDS (DevScene::top_mesh) and walks the other from
+    node_kids; megakernel and wavefront against the oracle at the 1e-9 / RGB8 bounds."""
+    import os
+    from test_host_prep import EXTRA_ASSET_SCENE, REPO
+
+    d = tmp_path / "two"
+    d.mkdir()
+    os.symlink(os.path.join(REPO, "scenes", "assets"), d / "assets")
+    chair = EXTRA_ASSET_SCENE.format(asset="chair.obj", scale=30.0, ty=24.5)
+    crew = EXTRA_ASSET_SCENE.format(asset="crewmate.obj", scale=0.25, ty=-73.7)
+    mesh_obj = crew[crew.index("[[objects]]\nbrdf = { type = \"diffuse\", kd = [0.8, 0.7, 0.5] }"):]
+    mesh_obj = mesh_obj[:mesh_obj.index("[[objects]]\nemitted")]
+    text = chair.replace("translate = [50.0,", "translate = [28.0,") + mesh_obj.replace("translate = [50.0,", "translate = [72.0,")
+    p = d / "s.toml"
+    p.write_text(text)
+    sc, orc = rt.Scene.from_toml(str(p)), oracle.OracleScene(str(p))
+    assert len(sc.mesh(5)["kind"]) >= 64 and len(sc.mesh(7)["kind"]) >= 64  # both walked by the pool
+    w, h, spp = 64, 48, 8
+    rgb_o, sub_o, st_o = orc.render(w, h, spp, SEED)
+    for mk in (True, False):
+        rgb_g, sub_g, st = rt.render(sc, w, h, spp, SEED, megakernel=mk, want_sub=True)
+        assert 0.9 * st_o["vertices"] <= st["vertices"] <= st_o["vertices"]
+        _assert_parity(rgb_g, sub_g, rgb_o, sub_o, f"two meshes/{'mk' if mk else 'wf'}")
+
+
 # ---------------------------------------------------------------- reference quirks off the 3 scenes
 QUIRK_SCENE = """
 [camera]
