@@ -115,12 +115,31 @@ struct ShadowDefer {
     double dist;
 };
 
+// Where a path keeps the two values only a mirror bounce hands on to the next vertex (read there only
+// when ps.kind == K_SPEC): `o`, the direction the reference passes on unchanged (scene.rs:178), and
+// the throughput before the bounce (Le(x') weight). RegCold: PathState's registers. LdsCold: a column
+// of LDS per thread (the analytic megakernel: 12 VGPRs of loop-carried state less; written only at
+// mirror bounces, read only after them).
+struct RegCold {
+    RT_DEV V3 o(const PathState& ps) const { return ps.o; }
+    RT_DEV void set_o(PathState& ps, V3 v) const { ps.o = v; }
+    RT_DEV V3 bemit(const PathState& ps) const { return ps.bemit; }
+    RT_DEV void set_bemit(PathState& ps, V3 v) const { ps.bemit = v; }
+};
+struct LdsCold {
+    __attribute__((address_space(3))) double* p;  // this thread's column of [6][256]
+    RT_DEV V3 o(const PathState&) const { return v3(p[0], p[256], p[512]); }
+    RT_DEV void set_o(PathState&, V3 v) const { p[0] = v.x; p[256] = v.y; p[512] = v.z; }
+    RT_DEV V3 bemit(const PathState&) const { return v3(p[768], p[1024], p[1280]); }
+    RT_DEV void set_bemit(PathState&, V3 v) const { p[768] = v.x; p[1024] = v.y; p[1280] = v.z; }
+};
+
 // Shades the hit `hr` of ps.ray. Returns true when the path continues (ps.ray is the next ray to
 // trace), false when this sample's radiance ps.L is final. The shadow ray of next-event estimation
 // is traced inline.
-template <class C>
+template <class C, class Cold = RegCold>
 RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
-                         const HitRec& hr, ShadowDefer* defer = nullptr) {
+                         const HitRec& hr, ShadowDefer* defer = nullptr, const Cold& cold = Cold()) {
     if (hr.obj < 0) return false;  // no hit: R = 0 (scene.rs:157, :175, :233)
     RT_DBG_REGION(6);
     const DevObject& obj = sc.objects[hr.obj];
@@ -131,7 +150,7 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
     if (ps.kind == K_CAMERA) {
         ps.L = ld3(obj.emitted);
     } else if (ps.kind == K_SPEC) {
-        ps.L = ps.L + mult(ps.bemit, ld3(obj.emitted));
+        ps.L = ps.L + mult(cold.bemit(ps), ld3(obj.emitted));
     } else if (C::mis && hr.obj == sc.light && ps.pdf_prev > 0.0) {
         // MIS, BSDF strategy: emitted radiance with the balance-heuristic weight
         double cosl = dot(nrm, -ps.ray.d);
@@ -139,7 +158,8 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
         double wgt = ps.pdf_prev / (ps.pdf_prev + pdf_l);
         ps.L = ps.L + mult(ps.beta, ld3(obj.emitted) * wgt);
     }
-    if (ps.kind != K_SPEC) ps.o = -ps.ray.d;
+    V3 o = -ps.ray.d;  // the out direction, except after a mirror bounce (which keeps the previous one)
+    if (ps.kind == K_SPEC) o = cold.o(ps);
     ps.depth += 1;
     const double p = ps.depth <= (uint32_t)MAX_BOUNCES ? 1.0 : SURVIVAL_PROBABILITY;
     Rng rng(ps.r0, ps.r1);
@@ -153,9 +173,10 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
         if (!survive) return false;
         V3 i;
         double pdf;
-        brdf_sample<C>(obj, nrm, ps.o, rng, &i, &pdf);
-        V3 f = brdf_eval<C>(obj, nrm, ps.o, i);
-        ps.bemit = ps.beta;
+        brdf_sample<C>(obj, nrm, o, rng, &i, &pdf);
+        V3 f = brdf_eval<C>(obj, nrm, o, i);
+        cold.set_bemit(ps, ps.beta);
+        cold.set_o(ps, o);
         ps.beta = mult(ps.beta, f) * dot(nrm, i) / (pdf * p);
         ps.ray = Ray{x, i};
         ps.kind = K_SPEC;
@@ -185,7 +206,7 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
         // (mirror vertices have no NEE)
         V3 lef = (RT_OPT_LEF && (!C::phong || obj.brdf == BRDF_DIFFUSE))
                      ? ld3(obj.lef)
-                     : mult(ld3(sc.objects[sc.light].emitted), brdf_eval<C>(obj, nrm, ps.o, i));
+                     : mult(ld3(sc.objects[sc.light].emitted), brdf_eval<C>(obj, nrm, o, i));
         if (!is_zero(lef)) {  // a zero Le*f makes the term exactly 0: skip the shadow ray
             RT_DBG_REGION(9);
             double vis;
@@ -239,12 +260,15 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
     V3 wi;
     double pdf;
     RT_DBG_TSTART(t_bs);
-    brdf_sample<C>(obj, nrm, ps.o, rng, &wi, &pdf);
+    brdf_sample<C>(obj, nrm, o, rng, &wi, &pdf);
     RT_DBG_TEND(11, t_bs);
     ps.r0 = rng.s0;
     ps.r1 = rng.s1;
-    V3 f = brdf_eval<C>(obj, nrm, ps.o, wi);
-    if (spec) ps.bemit = ps.beta;  // Le(x') after a mirror bounce is weighted by the beta before it
+    V3 f = brdf_eval<C>(obj, nrm, o, wi);
+    if (spec) {  // Le(x') after a mirror bounce is weighted by the beta before it; o goes on unchanged
+        cold.set_bemit(ps, ps.beta);
+        cold.set_o(ps, o);
+    }
     ps.beta = mult(ps.beta, f) * dot(nrm, wi) / (pdf * p);
     ps.ray = Ray{x, wi};
     ps.kind = spec ? K_SPEC : K_DIFF;

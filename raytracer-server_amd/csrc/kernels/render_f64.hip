@@ -33,6 +33,9 @@ typedef __attribute__((address_space(3))) uint64_t LdsU64;
 #ifndef RT_OPT_LDSOBJ
 #define RT_OPT_LDSOBJ 1  // A/B: the object table in LDS (per-lane object reads as ds_read)
 #endif
+#ifndef RT_OPT_COLD
+#define RT_OPT_COLD 1  // A/B: mirror-bounce state (o, pre-bounce throughput) in LDS (LdsCold) or registers
+#endif
 
 template <int F, int W>
 __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
@@ -59,6 +62,12 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
     // ended each iteration otherwise runs every iteration at that lane utilisation).
     __shared__ double s_acc[3 * 256], s_nbd[kCamDepth * 3 * 256];
     __shared__ uint64_t s_nbr[kCamDepth * 2 * 256];
+#if RT_OPT_COLD
+    __shared__ double s_cold[6 * 256];  // integrator_f64.h LdsCold: o and the pre-bounce throughput of mirror paths
+    const LdsCold cold{(LdsDouble*)s_cold + threadIdx.x};
+#else
+    const RegCold cold{};
+#endif
     LdsDouble* acc_l = (LdsDouble*)s_acc + threadIdx.x;  // component k at [k * 256]
     LdsDouble* nbd = (LdsDouble*)s_nbd + threadIdx.x;     // slot q, component k at [(q * 3 + k) * 256]
     LdsU64* nbr = (LdsU64*)s_nbr + threadIdx.x;           // slot q, word k at [(q * 2 + k) * 256]
@@ -126,7 +135,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
             RT_DBG_TEND(2, t_tr);
             nverts += hr.obj >= 0;
             RT_DBG_TSTART(t_sh);
-            fresh = !shade_vertex<C>(sc, a, ps, hr);
+            fresh = !shade_vertex<C>(sc, a, ps, hr, nullptr, cold);
             RT_DBG_TEND(3, t_sh);
             RT_DBG_TSTART(t_se);
             if (fresh) {
