@@ -505,9 +505,10 @@ __shared__ unsigned long long s_dbg_time[4 * 16];
 // opens a leaf or descends and masks the new node's children), so a wave can interleave walks of
 // different lengths and refill lanes whose walk ended (persistent traversal kernels).
 #ifndef RT_LTRI_INDEX
-#define RT_LTRI_INDEX 0  // 1: leaf triangle lists as indices into DevScene::tris instead of per-leaf copies
-                         // (3.6 MB instead of 18 MB for the unicorn, but one more dependent load per
-                         // triangle: measured 3% slower)
+#define RT_LTRI_INDEX 0  // 1: leaf triangle lists as indices into DevScene::tris (3.6 MB for the unicorn);
+                         // 0: per-leaf copies (18 MB). The index adds a dependent load per triangle: 3%
+                         // slower while tri_t loaded triangles one by one, 0.5% once a step's triangles
+                         // are preloaded (profiles/r02_ab.log): the copies stay the default
 #endif
 struct OctWalk {
     double mn[3], mx[3];  // box of `cur`
@@ -610,21 +611,28 @@ constexpr int kTrisPerStep = RT_TRIS_PER_STEP;
 #define RT_TRI_PRELOAD 1  // A/B: the step's triangles are loaded whole before any test (1), or by tri_t (0)
 #endif
 RT_DEV int leaf_tris(const DevScene& sc, const Ray& ray, OctWalk& w, double* t, int* prim) {
-#if RT_TRI_PRELOAD && !RT_LTRI_INDEX
+#if RT_TRI_PRELOAD
     // All of the step's triangles (96 B each) are loaded up front: tri_t reads a triangle's normal,
     // tests |n . d| and only then its other 72 B, and the next triangle only after that, i.e. four
     // dependent trips to L2 / the Infinity Cache per step. Entries past the leaf's end are clamped
     // to its last one (loaded, never tested).
     DevTri tr[kTrisPerStep];
 #pragma unroll
-    for (int j = 0; j < kTrisPerStep; ++j) tr[j] = sc.ltris[max(0, min(w.lpos + j, w.lend - 1))];
+    for (int j = 0; j < kTrisPerStep; ++j) {
+        const int e = max(0, min(w.lpos + j, w.lend - 1));
+#if RT_LTRI_INDEX
+        tr[j] = sc.tris[sc.ltri_id[e]];
+#else
+        tr[j] = sc.ltris[e];
+#endif
+    }
 #endif
 #pragma unroll
     for (int j = 0; j < kTrisPerStep; ++j) {
         if (w.lpos < w.lend) {
             RT_DBG(4);
             double tt;
-#if RT_TRI_PRELOAD && !RT_LTRI_INDEX
+#if RT_TRI_PRELOAD
             if (tri_t(tr[j], ray, &tt) && (w.best < 0 || tt < w.bt)) {
 #else
 #if RT_LTRI_INDEX
