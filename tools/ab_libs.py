@@ -20,7 +20,8 @@ for r in range(rounds):
     for lib in (libs if r % 2 == 0 else libs[::-1]):
         path = os.path.join(REPO, "raytracer-server_amd", "lib", "librtamd.so") if lib == "main" else os.path.join(REPO, lib)
         env = dict(os.environ, RT_AMD_LIB=path)
-        out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "prof_render.py"), scene, w, h, spp, "mk", *extra],
+        out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "prof_render.py"), scene, w, h, spp,
+                              os.environ.get("AB_MODE", "mk"), *extra],
                              env=env, capture_output=True, text=True, timeout=600)
         line = out.stdout.strip().splitlines()[-1] if out.stdout.strip() else out.stderr[-400:]
         m = re.search(r"([\d.]+) Msamples/s", line)
