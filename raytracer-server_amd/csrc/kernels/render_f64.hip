@@ -868,7 +868,8 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, dou
     static const int interleave = env_int("RT_MK_INTERLEAVE", 64);
     static const int ksteps = std::max(1, env_int("RT_MK_KSTEPS", 4));
     // camera-sample buffer refill threshold (lanes per wave; 0 disables the buffer)
-    static const int refill = env_int("RT_MK_CAM_REFILL", 24);
+    // (24 until round 2; 32-48 measured +0.6-0.9% on cornell, profiles/r02_ab.log)
+    static const int refill = env_int("RT_MK_CAM_REFILL", 40);
     static const int wmin = std::max(1, env_int("RT_MK_WALK_MIN", 1));
     static const int bvh_fused = env_int("RT_MK_BVH_FUSED", 0);  // A/B: nearest-triangle mode without interleaving
     // scenes whose meshes are all flat octrees (the cubes): block-synchronous batched mesh queries
