@@ -11,25 +11,28 @@ fixed: scaling = "strong". Rank 0 prints one JSON line.
 
 roofline (dominant kernel = the render megakernel; kernel_ms = its average device time per launch,
 HIP events recorded on the stream the kernel runs on):
-  * bound "hbm": achieved = the HBM bytes the PMC counters measured for one launch of this exact
-    workload (profiles/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE, separate rocprofv3 passes over
-    `bench.py --steps 1 --warmup 0`, tools/gpu_task.sh benchpmc) / kernel_ms; peak 8.0 TB/s;
-    traffic = those bytes; null when no measurement exists for the workload;
-  * algorithmic_bytes_per_launch = the megakernel's own unavoidable traffic: the f64 subpixel means
+  * bound "hbm" with SURVEY §8(d)'s algorithmic bytes, the figure §8(d) names for roofline.achieved:
+    88 B per camera sample + 280 B per path vertex (the canonical f32 SoA wavefront's state traffic;
+    vertices = this run's device counter) over kernel_ms; peak 8.0 TB/s; frac = achieved / peak.
+    The megakernel does not stream that state (a path lives in registers), so this is the rate the
+    kernel's throughput corresponds to on §8(d)'s roofline, not bytes it moves;
+  * traffic = the HBM bytes the PMC counters measured for one launch of this exact command
+    (profiles/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE, separate rocprofv3 passes over
+    `bench.py --steps 1 --warmup 0`, tools/gpu_task.sh benchpmc), scaled to this rank's rows; null
+    when no measurement exists for the workload. measured_frac = traffic / kernel_ms / peak;
+  * minimum_bytes_per_launch = the megakernel's own unavoidable traffic: the f64 subpixel means
     written (4 x 3 x 8 B per pixel) and read back by the finalize, plus the RGB8 frame;
-  * wavefront_equiv_frac = SURVEY §8(d)'s canonical model (88 B per camera sample + 280 B per path
-    vertex of an f32 SoA wavefront) over kernel_ms / 8 TB/s: what the same throughput would stream
-    as a wavefront — a model, not a measurement;
-  * compute = the kernel's real bound, f64 VALU issue: the PMC instruction mix per path vertex of
-    this scene and mode (profiles/pmc_valu.json, tools/pmc_report.py) priced per class on a SIMD-32
-    (f64 add/mul/fma 4 cycles per wave64 instruction, f64 transcendental 8, 64-bit integer 4, other
-    VALU 2) times this run's vertex rate, over 1024 SIMDs x the PMC-measured clock; and the FP64
-    FLOP rate against 78.6 TFLOP/s.
+  * binds = what limits the kernel: f64 VALU issue (the block "compute"): the PMC instruction mix per
+    path vertex of this command (profiles/pmc_valu.json, SQ passes of benchpmc, tools/pmc_report.py)
+    priced per class on a SIMD-32 (f64 add/mul/fma 4 cycles per wave64 instruction, f64
+    transcendental 8, 64-bit integer 4, other VALU 2) times this run's vertex rate, over 1024 SIMDs x
+    the PMC-measured clock; and the FP64 FLOP rate against 78.6 TFLOP/s.
 
 cpu_baseline: the CPU oracle (a line-by-line f64 restatement of the reference's sample loop; the
 reference itself is Rust and cannot be built here), compiled on this host with -O3 -march=native,
-on a bounded row band of the same frame on min(16, cpu_count) threads, and on 1 thread; rank 0 at
-N = 1 only.
+on a bounded row band of the same frame on every core this job may use (host_cores(): the cgroup CPU
+quota, else the pool's declared share OMP_NUM_THREADS, else the affinity mask; os.cpu_count() is
+reported beside it), and on 1 thread; rank 0 at N = 1 only.
 """
 import argparse
 import hashlib
@@ -111,6 +114,33 @@ def native_oracle():
         return None, "-O3 (portable build; -march=native compile failed)"
 
 
+def host_cores():
+    """(cores, source): the CPU share this job may use. A GPU box shows the whole machine's CPUs in
+    os.cpu_count() / nproc but grants a job a share of them (cgroup quota, or the pool's declared
+    OMP_NUM_THREADS); threads beyond the share only time-slice."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) // int(per))), "cgroup cpu.max"
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        if q > 0:
+            return max(1, q // per), "cgroup cfs quota"
+    except (OSError, ValueError):
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < aff:
+        return int(omp), "OMP_NUM_THREADS (the pool's CPU share per GPU job)"
+    return aff, "sched_getaffinity"
+
+
 def cpu_baseline(args):
     lib, flags = native_oracle()
     if lib:
@@ -118,7 +148,7 @@ def cpu_baseline(args):
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_bind
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, cores_source = host_cores()
     sc = oracle_bind.OracleScene(os.path.join(REPO, "scenes", f"{args.scene}.toml"))
     rows = min(args.cpu_rows, args.height)
     y0 = (args.height - rows) // 2
@@ -138,6 +168,7 @@ def cpu_baseline(args):
     if lib:
         os.unlink(lib)
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "cores_source": cores_source, "host_cpus_visible": os.cpu_count(),
             "sample": f"{args.scene} rows {y0}..{y0 + rows} of {args.width}x{args.height} at {args.cpu_spp} spp "
                       f"({samples} samples, {dt:.1f} s, f64, CPU oracle restating server.rs:320-368 + scene.rs + "
                       f"geometry.rs, g++ {flags})",
@@ -259,6 +290,7 @@ def main():
         traffic = int(traffic_full * th / args.height) if traffic_full else None
         achieved = traffic / (dev_ms / 1e3) / 1e9 if traffic else None
         model_bytes = BYTES_PER_SAMPLE * rank_samples + BYTES_PER_VERTEX * st["vertices"]
+        model_gbs = model_bytes / (dev_ms / 1e3) / 1e9
         npix = args.width * th
         alg_bytes = npix * (2 * 12 * 8 + 3)  # f64 subpixel means written + read by the finalize, RGB8 out
         out = {
@@ -283,21 +315,26 @@ def main():
                        "parallelism": f"{'interleaved rows' if args.partition == 'interleave' else 'row stripes'} x{world}"
                                       ", host gather (gloo)" if world > 1 else "1 GPU",
                        "frame_sha1": digest,
+                       "vertices": total_vertices,
                        "vertices_per_sample": round(total_vertices / n_samples, 4)},
             "roofline": {"bound": "hbm",
-                         "achieved": round(achieved, 3) if achieved is not None else None,
+                         "achieved": round(model_gbs, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 6) if achieved is not None else None,
+                         "frac": round(model_gbs / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
+                         "algorithmic_bytes_per_launch": model_bytes,
+                         "algorithmic_model": "SURVEY 8(d): 88 B per camera sample + 280 B per path vertex (f32 SoA "
+                                              "wavefront state), vertices from this run's device counter",
+                         "kernel": kernel, "kernel_ms": round(dev_ms, 3),
+                         "measured_frac": round(achieved / HBM_PEAK_GBS, 6) if achieved is not None else None,
                          "traffic_source": "profiles/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE per launch, "
                                            "rocprofv3 passes over this command)" if traffic else None,
-                         "kernel": kernel, "kernel_ms": round(dev_ms, 3),
-                         "algorithmic_bytes_per_launch": alg_bytes,
-                         "wavefront_equiv_frac": round(model_bytes / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "wavefront_equiv_model": "SURVEY 8(d): 88 B/sample + 280 B/vertex (f32 SoA wavefront state), "
-                                                  "a model of what a wavefront would stream, not measured traffic"},
+                         "minimum_bytes_per_launch": alg_bytes,
+                         "binds": "valu_issue_f64" if args.mode == "megakernel" else "launches_and_state_traffic"},
         }
-        mix = load_profile("pmc_valu.json", f"{args.scene} {mode}{' mis' if args.mis else ''}")
+        # the instruction mix of this exact command (benchpmc), else of the scene's own PMC workload
+        mix = load_profile("pmc_valu.json", f"{workload} {mode}") or \
+            load_profile("pmc_valu.json", f"{args.scene} {mode}{' mis' if args.mis else ''}")
         if mix and args.mode == "megakernel":
             out["roofline"]["compute"] = compute_block(mix, st["vertices"], dev_ms)
         if world == 1 and not args.no_cpu_baseline:

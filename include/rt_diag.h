@@ -7,10 +7,16 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
-/* Device self-test of the exact-arithmetic shortcuts (path_f64.h: rcp_rn, qdiv) against IEEE
- * division on n pseudo-random operands on the current HIP device; out[0] = reciprocal mismatches,
- * out[1] = quotient mismatches. Returns 0 or -1 (HIP error). */
-int rt_selftest_arith(long n, unsigned long long seed, unsigned long long out[2]);
+/* Device self-test of the exact-arithmetic shortcuts (path_f64.h: rcp_rn, qdiv, sqrt_rn) against
+ * the IEEE operations on n pseudo-random operands on the current HIP device; out[0] = reciprocal
+ * mismatches, out[1] = quotient mismatches, out[2] = square-root mismatches (sqrt_rn's fast range
+ * [2^-767, 2^1024) against the library sqrt). Returns 0 or -1 (HIP error). */
+int rt_selftest_arith(long n, unsigned long long seed, unsigned long long out[3]);
+/* RT_QCHECK builds (-DRT_QCHECK=1): counters of LDS hand-off protocol violations in the megakernels'
+ * work queues since the last call (kernels/megakernel_common.h): [0] ring slot overwritten / bad
+ * entry, [1] queue over capacity, [2] outstanding-query count below zero, [3] owner/taker state
+ * mismatch. Returns 0, 1 when the checks are not compiled in (zeros), -1 on a HIP error. */
+int rt_debug_qcheck(unsigned long long out[4]);
 /* RT_DEBUG_COUNTERS builds: octree traversal counters since the last call (zeros otherwise):
  * [0] walks [1] past the cull [2] node visits [3] leaves opened [4] triangle tests [5] walk steps;
  * interleaved mesh megakernel: [8] wave iterations [9] lanes in the vertex phase [10] walk-loop

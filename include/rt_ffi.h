@@ -134,8 +134,10 @@ int rt_scene_mesh(const rt_scene* scene, int32_t object, int64_t counts[4] /* no
 
 /* Rendering ------------------------------------------------------------------------------- */
 /* Host buffers: rgb_out tile_w*tile_h*3 u8; sub_out (optional) tile_w*tile_h*4*3 f64 subpixel
- * means before the clamp; cancel (optional) polled between bounce iterations (nonzero = stop,
- * returns RT_CANCELLED). stats optional. */
+ * means before the clamp; cancel (optional; nonzero = stop, returns RT_CANCELLED): read by the
+ * calling thread while the render runs and copied into a pinned word the megakernels poll between
+ * subpixels (the wavefront: between bounce batches). The flag is never registered with HIP and may be
+ * shared by concurrent renders. stats optional. */
 int rt_render(const rt_scene* scene, const rt_render_params* params, uint8_t* rgb_out, double* sub_out,
               const volatile int32_t* cancel, rt_render_stats* stats);
 /* Device buffers on params->device; enqueued on `stream` (hipStream_t, NULL = default stream).
@@ -149,7 +151,8 @@ int rt_render_device(const rt_scene* scene, const rt_render_params* params, void
  * (an ordinal may repeat: several workers on one device). A worker renders each band with the device path on
  * its own streams (two bands in flight, so one band's tail overlaps the next band's start) and copies the RGB8
  * rows straight into rgb_out: the gather is host-side, no collective. The image is byte-identical to rt_render
- * of the same params (the RNG is keyed by global pixel). cancel is checked between bands. stats (optional):
+ * of the same params (the RNG is keyed by global pixel). cancel is checked between bands and relayed to
+ * the running bands' kernels as in rt_render. stats (optional):
  * samples and vertices summed over the bands, device_ms = wall time of the whole call. */
 int rt_render_multi(const rt_scene* scene, const rt_render_params* params, const int32_t* devices, int32_t n_devices,
                     int32_t band_rows, uint8_t* rgb_out, const volatile int32_t* cancel, rt_render_stats* stats);

@@ -656,13 +656,12 @@ RT_DEV int leaf_tris(const DevScene& sc, const Ray& ray, OctWalk& w, double* t, 
     }
     return -1;
 }
-RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w, double* t,
-                     int* prim, const LdsTopI32* top = nullptr) {
-    RT_DBG(5);
-    if (w.lpos < w.lend) {  // triangles of the open leaf
-        const int st = leaf_tris(sc, ray, w, t, prim);
-        if (st >= 0) return st;
-    }
+// The node part of a walk step (no leaf open, or its triangles exhausted without a hit): pops every
+// exhausted level, then picks the next child in visiting order and either opens it (a leaf: its
+// triangle range in w.lpos / w.lend) or descends into it and masks its children (walk_enter).
+// WALK_RUN, or WALK_MISS once the root is exhausted.
+RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w,
+                     const LdsTopI32* top = nullptr) {
     if (w.pm == 0) {  // `cur` exhausted: resume at the nearest ancestor with children left
         int lv = w.depth;
         uint32_t pm = 0;
@@ -714,12 +713,7 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         w.lpos = first;
         w.lend = first + cnt;
         w.best = -1;
-#if RT_WALK_OPEN_TEST
-        const int st = leaf_tris(sc, ray, w, t, prim);
-        return st >= 0 ? st : WALK_RUN;
-#else
         return WALK_RUN;
-#endif
     }
     // descend: push the remaining mask of `cur`, take the octant's box
     const int lv = w.depth;
@@ -735,6 +729,22 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
     }
     walk_enter(sc, ray, inv, w, top);
     return WALK_RUN;
+}
+RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w, double* t,
+                     int* prim, const LdsTopI32* top = nullptr) {
+    RT_DBG(5);
+    if (w.lpos < w.lend) {  // triangles of the open leaf
+        const int st = leaf_tris(sc, ray, w, t, prim);
+        if (st >= 0) return st;
+    }
+    const int st = walk_node(sc, m, ray, inv, w, top);
+#if RT_WALK_OPEN_TEST
+    if (st == WALK_RUN && w.lpos < w.lend) {  // a leaf was just opened: its first triangles in this step
+        const int s2 = leaf_tris(sc, ray, w, t, prim);
+        return s2 >= 0 ? s2 : WALK_RUN;
+    }
+#endif
+    return st;
 }
 
 // Mesh::intersect's `octree: None` branch (geometry.rs:886-903): the nearest triangle hit, strict <

@@ -63,6 +63,8 @@ struct alignas(16) DevMesh {
     uint32_t flat_leaf[8];
 };
 constexpr int kFlatMaxTris = 32;
+constexpr int kFlatMeshes = 2;  // meshes of a flat scene: the flat kernels' LDS queues and result columns
+                                // (render_flat_f64.hip) and rt_api.cpp's RenderArgs::all_flat
 
 // BVH over a mesh's triangles for the nearest-triangle mode (RT_FLAG_MESH_NEAREST), nodes in DFS
 // pre-order: an inner node's left child is the next node, `a` its right child, `axis` the split

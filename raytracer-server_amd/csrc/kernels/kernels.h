@@ -38,10 +38,18 @@ struct RenderArgs {
 // tail_buf / tail_cap: scratch for the split tail (bytes); the launcher sizes the tail to fit it.
 hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
                                  double* tail_buf, size_t tail_cap, hipStream_t st);
-// Block-synchronous kernel for flat-octree mesh scenes (render_flat_f64.hip); called by
+// Query-pool kernel for flat-octree mesh scenes (render_flat_f64.hip); called by
 // launch_megakernel_f64 after the ticket counter is reset.
 hipError_t launch_megakernel_flat_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
                                       double* tail_buf, size_t tail_cap, int refill, hipStream_t st);
+// Deep-octree mesh megakernel (render_mesh_f64.hip, walk pool); called by launch_megakernel_f64 after
+// the ticket counter is reset; a: the caller's args (features, sizes), planned here.
+hipError_t launch_megakernel_mesh_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
+                                      long nsub, int refill, int wmin, double* tail_buf, size_t tail_cap, hipStream_t st);
+// Diagnostic symbols of each kernel code object (diag_tu.h): read, add to the outputs, clear.
+int diag_read_main(unsigned long long* cnt16, unsigned long long* reg32, unsigned long long* tim16, unsigned long long* q4);
+int diag_read_mesh(unsigned long long* cnt16, unsigned long long* reg32, unsigned long long* tim16, unsigned long long* q4);
+int diag_read_flat(unsigned long long* cnt16, unsigned long long* reg32, unsigned long long* tim16, unsigned long long* q4);
 // f32 perf mode (render_f32.hip): writes the subpixel means to sub_buf like the f64 megakernel.
 hipError_t launch_megakernel_f32(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
                                  hipStream_t st);

@@ -70,6 +70,23 @@ __device__ __forceinline__ bool unit_has_next(const RenderArgs& a, int id, int s
 
 __device__ __forceinline__ bool lane_id_is0() { return __lane_id() == 0; }
 
+// Protocol checks of the LDS hand-offs below (build with -DRT_QCHECK=1; rt_debug_qcheck reads and
+// clears them). A violation is counted, never trapped (a trap would fault the device):
+//   [0] queue_put found its ring slot still holding an entry (not -1), or queue_read a value that is
+//       not a queue entry;  [1] more entries queued than the ring holds (tail - head > capacity);
+//   [2] an outstanding-query count (fpool s_pend) decremented below zero;
+//   [3] an owner / taker state mismatch: a new count stored over a non-zero s_pend, or the walk pool
+//       handing out a query whose status word is not CLOSEST / SHADOW.
+#ifndef RT_QCHECK
+#define RT_QCHECK 0
+#endif
+#if RT_QCHECK
+__device__ unsigned long long g_qcheck[4];
+#define RT_QFAIL(i) atomicAdd(&g_qcheck[i], 1ull)
+#else
+#define RT_QFAIL(i) ((void)0)
+#endif
+
 // Multi-producer multi-consumer work queue of int entries (>= 0) in LDS, shared by the waves of a
 // block without barriers: a ring of mask + 1 entries (initialised to -1) with monotonically growing
 // head / tail counters. The caller guarantees that no more than mask + 1 entries are ever queued
@@ -81,9 +98,11 @@ struct LdsQueue {
     uint32_t* tail;  // next entry to fill
     uint32_t mask;   // capacity - 1 (a power of two)
 };
+// Entries queued and not yet claimed (head read first: the tail read after it is >= it, so the
+// difference never wraps).
 __device__ __forceinline__ uint32_t queue_len(const LdsQueue& q) {
-    return __hip_atomic_load(q.tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) -
-           __hip_atomic_load(q.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t h = __hip_atomic_load(q.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __hip_atomic_load(q.tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) - h;
 }
 // Appends v of every lane with `put` (wave-aggregated). All lanes of the wave call.
 __device__ __forceinline__ void queue_put(const LdsQueue& q, bool put, int32_t v) {
@@ -95,7 +114,20 @@ __device__ __forceinline__ void queue_put(const LdsQueue& q, bool put, int32_t v
     if (lane == leader) base = __hip_atomic_fetch_add(q.tail, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     base = __shfl(base, leader, 64);
     const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+#if RT_QCHECK
+    if (lane == leader) {
+        const uint32_t h = __hip_atomic_load(q.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // signed: takers may already have claimed past this append (head > base + n) while it is written
+        if ((int32_t)(base + (uint32_t)__popcll(m) - h) > (int32_t)(q.mask + 1u)) RT_QFAIL(1);
+    }
+    if (put) {
+        const int32_t old = __hip_atomic_exchange(&q.ring[(base + (uint32_t)__popcll(below)) & q.mask], v, __ATOMIC_RELEASE,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (old != -1) RT_QFAIL(0);
+    }
+#else
     if (put) __hip_atomic_store(&q.ring[(base + (uint32_t)__popcll(below)) & q.mask], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
 }
 // Claims up to `most` entries, but only if at least max(need, 1) are queued; the leader lane does the
 // compare-and-swap. Returns the first claimed position and the count (wave-uniform).
@@ -123,6 +155,7 @@ __device__ __forceinline__ int32_t queue_read(const LdsQueue& q, uint32_t pos) {
     int32_t v;
     while ((v = __hip_atomic_load(e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < 0) __builtin_amdgcn_s_sleep(1);
     __hip_atomic_store(e, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (RT_QCHECK && (uint32_t)v > q.mask) RT_QFAIL(0);  // entries (lane ids, + 256 for fpool shadow queries) < capacity
     return v;
 }
 // Takes up to 64 entries (lane i the i-th), but only if at least `need` are queued; -1 for lanes

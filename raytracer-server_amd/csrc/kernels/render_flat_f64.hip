@@ -20,9 +20,7 @@
 //      query pending waits one iteration (no new path in A) until C has its result.
 // Every query returns the same bits as the per-lane walk (same tri_t, same box_hit per octant, same
 // visiting order), so frames are identical to k_megakernel_f64's and the wavefront's (tested).
-// Included by render_f64.hip (one code object: the diagnostic counters of path_f64.h are per code
-// object).
-#pragma once
+// Its own translation unit (code object): launched by launch_megakernel_f64 (render_f64.hip).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -37,7 +35,6 @@ using namespace f64;
 
 namespace {
 
-constexpr int kFlatMeshes = 2;  // meshes of a flat scene (LDS queues; rt_api.cpp: RenderArgs::all_flat)
 constexpr int kBlk = 256;
 typedef __attribute__((address_space(3))) double LdsD;
 typedef __attribute__((address_space(3))) uint64_t LdsU;
@@ -591,7 +588,8 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                     } else {
                         s_ro[m * kBlk + who] = hit && !(t + 0.001 >= q[6 * kBlk + who]) ? 1 : 0;
                     }
-                    __hip_atomic_fetch_sub(&s_pend[who], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const int32_t left = __hip_atomic_fetch_sub(&s_pend[who], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (RT_QCHECK && left <= 0) RT_QFAIL(2);
                 }
             }
         }
@@ -727,6 +725,8 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
             traced = true;
         }
         // queue this lane's new queries (its s_pend is 0 until they are queued: nobody else writes it)
+        if (RT_QCHECK && (want_s | want_c) && __hip_atomic_load(&s_pend[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
+            RT_QFAIL(3);
         if (want_s | want_c) s_pend[tid] = __popc(want_s) + __popc(want_c);
         for (int m = 0; m < nm; ++m) {
             const LdsQueue Q{s_ring[m], &s_head[m], &s_tail[m], (uint32_t)kFpRing - 1u};
@@ -782,5 +782,8 @@ hipError_t launch_megakernel_flat_f64(const DevScene& sc, const RenderArgs& a_in
     launch_tail_sum_f64(a, sub_buf, nsub - a.n_whole, st);
     return hipGetLastError();
 }
+
+#define RT_DIAG_TU_FN diag_read_flat
+#include "diag_tu.h"
 
 }  // namespace rt

@@ -1,0 +1,751 @@
+// f64 megakernel for scenes with deep triangle-mesh octrees (flying_unicorn): octree walks
+// (Mesh::intersect, geometry.rs:883-905, 1237-1295) interleaved with path vertices, by default through
+// the block's walk pool. Its own translation unit (code object): launched by launch_megakernel_f64
+// (render_f64.hip) through launch_megakernel_mesh_f64.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+
+#include "../device/integrator_f64.h"
+#include "kernels.h"
+#include "megakernel_common.h"
+
+namespace rt {
+using namespace f64;
+
+typedef __attribute__((address_space(3))) double LdsDouble;
+typedef __attribute__((address_space(3))) int32_t LdsInt;
+typedef __attribute__((address_space(3))) uint64_t LdsU64;
+#ifndef RT_OPT_LDSOBJ
+#define RT_OPT_LDSOBJ 1  // A/B: the object table in LDS (per-lane object reads as ds_read)
+#endif
+
+// Begins the octree walk of the next candidate mesh after gen slot g (Scene::trace_ray's /
+// mutually_visible's loop over the mesh objects); false when no mesh is left.
+// `top`: the LDS copy of mesh sc.top_mesh's top levels (walk-pool kernel), or null.
+template <class C>
+RT_DEV bool next_mesh_walk(const DevScene& sc, const Ray& r, const RayInv& inv, double tmax, int& g, int& mi,
+                           OctWalk& w, const LdsTopI32* top = nullptr) {
+    for (++g; g < tables(sc)->n_gen; ++g) {
+        const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
+        if (o.geom == GEOM_MESH &&
+            walk_begin(sc, sc.meshes[o.mesh], r, inv, tmax, w, o.mesh == sc.top_mesh ? top : nullptr)) {
+            mi = o.mesh;
+            return true;
+        }
+    }
+    return false;
+}
+
+// Megakernel for scenes with triangle meshes: octree walks interleaved with path vertices.
+// A walk is long-tailed (tens of steps for the few rays that reach the mesh's box; none for the
+// rest), so tracing it to completion inside the vertex makes every lane of the wave wait for the
+// wave's longest walk. Here a lane whose ray needs a mesh walk parks its path and walks
+// `ksteps` steps per iteration (walk_step is resumable), while the other lanes of the wave keep
+// shading vertices; a lane rejoins the vertex work the iteration its walk ends. The walk queries
+// are the wavefront's deferred ones (closest: the analytic hit, then the meshes in gen order with
+// the reference's tie rule; shadow: the analytic objects let the ray through, then any mesh may
+// block it), so every path produces the same bits as k_megakernel_f64 (tested).
+enum : int { PH_TRACE = 0, PH_WALK_CLOSEST = 1, PH_WALK_SHADOW = 2 };
+
+// The walk state of each lane lives in LDS between walk phases ("parked"), one column per thread
+// of the block, so the vertex phase runs with the register footprint of the analytic kernel and
+// the walk phase holds only the path state plus the walk (no scratch spills at 2 waves/SIMD).
+// Doubles: ray o, d; 1/d; box mn, mx; walk best t; query t (closest hit so far / shadow distance);
+// pending NEE term. Ints: walk cursor fields, closest hit object/prim, gen slot, mesh, occluded.
+constexpr int kParkD = 21, kParkI = 16, kParkThreads = 256;
+struct Park {  // typed in the LDS address space: ds_read/ds_write with one 32-bit base + immediate offsets
+    LdsDouble* d;  // this thread's column of [kParkD][kParkThreads]
+    LdsInt* i;     // [kParkI][kParkThreads]
+    RT_DEV LdsDouble& D(int f) const { return d[f * kParkThreads]; }
+    RT_DEV LdsInt& I(int f) const { return i[f * kParkThreads]; }
+};
+struct WalkRegs {  // the walk phase's working copy
+    Ray wr;
+    RayInv wi;
+    OctWalk w;
+    double wt;  // closest: hit t so far (h.t); shadow: |y - x|
+    int32_t hobj, hprim, g, mi, occluded;
+};
+RT_DEV void park_store(const Park& p, const WalkRegs& r) {
+    p.D(0) = r.wr.o.x; p.D(1) = r.wr.o.y; p.D(2) = r.wr.o.z;
+    p.D(3) = r.wr.d.x; p.D(4) = r.wr.d.y; p.D(5) = r.wr.d.z;
+    p.D(6) = r.wi.rx; p.D(7) = r.wi.ry; p.D(8) = r.wi.rz;
+    for (int k = 0; k < 3; ++k) { p.D(9 + k) = r.w.mn[k]; p.D(12 + k) = r.w.mx[k]; }
+    p.D(15) = r.w.bt;
+    p.D(16) = r.wt;
+    p.I(0) = r.w.cur; p.I(1) = r.w.depth; p.I(2) = (int32_t)r.w.path; p.I(3) = (int32_t)r.w.pm;
+    p.I(4) = (int32_t)(uint32_t)r.w.stk; p.I(5) = (int32_t)(uint32_t)(r.w.stk >> 32); p.I(6) = (int32_t)r.w.stk8;
+    p.I(7) = (int32_t)r.w.order; p.I(8) = r.w.lpos; p.I(9) = r.w.lend; p.I(10) = r.w.best;
+    p.I(11) = r.hobj; p.I(12) = r.hprim; p.I(13) = r.g; p.I(14) = r.mi; p.I(15) = r.occluded;
+}
+RT_DEV void park_load(const Park& p, WalkRegs& r) {
+    r.wr.o = v3(p.D(0), p.D(1), p.D(2));
+    r.wr.d = v3(p.D(3), p.D(4), p.D(5));
+    r.wi.rx = p.D(6); r.wi.ry = p.D(7); r.wi.rz = p.D(8);
+    for (int k = 0; k < 3; ++k) { r.w.mn[k] = p.D(9 + k); r.w.mx[k] = p.D(12 + k); }
+    r.w.bt = p.D(15);
+    r.wt = p.D(16);
+    r.w.cur = p.I(0); r.w.depth = p.I(1); r.w.path = (uint32_t)p.I(2); r.w.pm = (uint32_t)p.I(3);
+    r.w.stk = (uint64_t)(uint32_t)p.I(4) | ((uint64_t)(uint32_t)p.I(5) << 32); r.w.stk8 = (uint32_t)p.I(6);
+    r.w.order = (uint32_t)p.I(7); r.w.lpos = p.I(8); r.w.lend = p.I(9); r.w.best = p.I(10);
+    r.hobj = p.I(11); r.hprim = p.I(12); r.g = p.I(13); r.mi = p.I(14); r.occluded = p.I(15);
+}
+
+// Nearest-triangle mode (Cfg::bvh): the BVH walk parks cur / sp / best / bt in the octree walk's
+// slots I(0), I(1), I(10), D(15), and its stack in the slots the octree walk would use for its
+// cursor (I(2..9)) and box (D(9..14) as int pairs): kBvhMaxDepth = 20 entries.
+struct ParkStack {
+    const Park& p;
+    RT_DEV LdsInt& at(int e) const {
+        return e < 8 ? p.I(2 + e) : ((LdsInt*)&p.D(9 + ((e - 8) >> 1)))[(e - 8) & 1];
+    }
+};
+static_assert(kBvhMaxDepth <= 8 + 12, "BVH stack does not fit the park slots");
+struct WalkRegsBvh {
+    Ray wr;
+    RayInv wi;
+    BvhWalk w;
+    double wt;
+    int32_t hobj, hprim, g, mi, occluded;
+};
+RT_DEV void park_store_bvh(const Park& p, const WalkRegsBvh& r) {
+    p.D(0) = r.wr.o.x; p.D(1) = r.wr.o.y; p.D(2) = r.wr.o.z;
+    p.D(3) = r.wr.d.x; p.D(4) = r.wr.d.y; p.D(5) = r.wr.d.z;
+    p.D(6) = r.wi.rx; p.D(7) = r.wi.ry; p.D(8) = r.wi.rz;
+    p.D(15) = r.w.bt;
+    p.D(16) = r.wt;
+    p.I(0) = r.w.cur; p.I(1) = r.w.sp; p.I(10) = r.w.best;
+    p.I(11) = r.hobj; p.I(12) = r.hprim; p.I(13) = r.g; p.I(14) = r.mi; p.I(15) = r.occluded;
+}
+RT_DEV void park_load_bvh(const Park& p, WalkRegsBvh& r) {
+    r.wr.o = v3(p.D(0), p.D(1), p.D(2));
+    r.wr.d = v3(p.D(3), p.D(4), p.D(5));
+    r.wi.rx = p.D(6); r.wi.ry = p.D(7); r.wi.rz = p.D(8);
+    r.w.bt = p.D(15);
+    r.wt = p.D(16);
+    r.w.cur = p.I(0); r.w.sp = p.I(1); r.w.best = p.I(10);
+    r.hobj = p.I(11); r.hprim = p.I(12); r.g = p.I(13); r.mi = p.I(14); r.occluded = p.I(15);
+}
+// Begins the BVH walk of the next candidate mesh after gen slot g; false when no mesh is left.
+template <class C>
+RT_DEV bool next_mesh_walk_bvh(const DevScene& sc, const Ray& r, const RayInv& inv, double tmax, int& g, int& mi,
+                               BvhWalk& w) {
+    for (++g; g < tables(sc)->n_gen; ++g) {
+        const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
+        if (o.geom != GEOM_MESH) continue;
+        const DevMesh& m = sc.meshes[o.mesh];
+        if (m.bvh_n > 0 && near_box(m.cull_box, r, inv, m.cull_pad, tmax)) {
+            mi = o.mesh;
+            bvh_begin(m, tmax, w);
+            return true;
+        }
+    }
+    return false;
+}
+
+// A new walk query: ray, 1/d, query t (closest analytic hit / shadow distance) and hit so far; the
+// first walk step begins the walk of the first candidate mesh (w.cur = -1: no walk in progress).
+RT_DEV void park_query(const Park& p, const Ray& r, const RayInv& wi, double wt, int32_t hobj, int32_t hprim) {
+    p.D(0) = r.o.x; p.D(1) = r.o.y; p.D(2) = r.o.z;
+    p.D(3) = r.d.x; p.D(4) = r.d.y; p.D(5) = r.d.z;
+    p.D(6) = wi.rx; p.D(7) = wi.ry; p.D(8) = wi.rz;
+    p.D(16) = wt;
+    p.I(0) = -1;
+    p.I(11) = hobj; p.I(12) = hprim; p.I(13) = -1; p.I(15) = 0;
+}
+
+// One round of walk steps for the queries held by the lanes with `wk` (the query in park `pk`;
+// closest: the closest-hit query of Scene::trace_ray, else the shadow query of mutually_visible):
+// up to ksteps steps, after the first only while >= wmin lanes still walk. Returns, per lane,
+// whether its query finished; the results are then in pk (D16 t, I11 object, I12 prim, I15
+// occluded), otherwise the walk state is stored back into pk.
+template <class C>
+RT_DEV bool walk_round(const DevScene& sc, const Park& pk, const bool wk, const bool closest, int ksteps, int wmin) {
+    bool walking = wk, done = false;
+    if constexpr (C::bvh) {
+      if (__any(walking)) {
+        WalkRegsBvh r;
+        if (walking) park_load_bvh(pk, r);
+        const ParkStack stk{pk};
+        for (int k = 0; k < ksteps && (k == 0 ? __any(walking) : __popcll(__ballot(walking)) >= wmin); ++k) {
+            RT_DBG_WAVE(10, lane_id_is0());
+            RT_DBG_WAVE(11, walking);
+            if (walking) {
+                bool fin = false;
+                if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
+                    const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
+                    fin = !next_mesh_walk_bvh<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w);
+                } else {
+                    const bool shadow = !closest;
+                    const int st = bvh_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, stk, shadow ? r.wt : -1.0);
+                    if (st != WALK_RUN) {
+                        if (!shadow) {
+                            if (st == WALK_HIT) {
+                                HitRec h{r.wt, r.hobj, r.hprim};
+                                consider(h, r.w.bt, tables(sc)->gen_idx[r.g], r.w.best);
+                                r.wt = h.t;
+                                r.hobj = h.obj;
+                                r.hprim = h.prim;
+                            }
+                        } else {
+                            r.occluded = st == WALK_HIT && !(r.w.bt + 0.001 >= r.wt);  // mutually_visible
+                            fin = r.occluded;
+                        }
+                        r.w.cur = -1;  // next step: the next mesh, if any
+                    }
+                }
+                if (fin) {  // results for the vertex phase
+                    walking = false;
+                    done = true;
+                    pk.D(16) = r.wt;
+                    pk.I(11) = r.hobj;
+                    pk.I(12) = r.hprim;
+                    pk.I(15) = r.occluded;
+                }
+            }
+        }
+        if (walking) park_store_bvh(pk, r);
+      }
+    } else if (__any(walking)) {
+        WalkRegs r;
+        if (walking) park_load(pk, r);
+        // up to ksteps steps; after the first, only while at least wmin lanes still walk
+        for (int k = 0; k < ksteps && (k == 0 ? __any(walking) : __popcll(__ballot(walking)) >= wmin); ++k) {
+            RT_DBG_WAVE(10, lane_id_is0());
+            RT_DBG_WAVE(11, walking);
+            if (walking) {
+                bool fin = false;
+                if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
+                    const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
+                    fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w);
+                } else {
+                    double t;
+                    int prim;
+                    const int st = walk_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim);
+                    if (st != WALK_RUN) {
+                        if (closest) {
+                            if (st == WALK_HIT) {
+                                HitRec h{r.wt, r.hobj, r.hprim};
+                                consider(h, t, tables(sc)->gen_idx[r.g], prim);
+                                r.wt = h.t;
+                                r.hobj = h.obj;
+                                r.hprim = h.prim;
+                            }
+                        } else {
+                            r.occluded = st == WALK_HIT && !(t + 0.001 >= r.wt);  // mutually_visible's ERR_MARGIN
+                            fin = r.occluded;
+                        }
+                        r.w.cur = -1;  // next step: the next mesh, if any
+                    }
+                }
+                if (fin) {  // results for the vertex phase
+                    walking = false;
+                    done = true;
+                    pk.D(16) = r.wt;
+                    pk.I(11) = r.hobj;
+                    pk.I(12) = r.hprim;
+                    pk.I(15) = r.occluded;
+                }
+            }
+        }
+        if (walking) park_store(pk, r);
+    }
+    return done;
+}
+
+// Walk pool (P = true): the walk queries of a block go through one LDS work queue (LdsQueue,
+// megakernel_common.h) instead of being walked by the lane that owns the path. A wave takes up to 64
+// runnable queries from the queue (any owner's), walks them for `ksteps` steps, hands finished
+// results to their owners (status word) and puts unfinished queries back. Walk steps then run with
+// the block's queries packed into full waves instead of the ~27 walking lanes of the wave that owns
+// them (the deep octree's walks are 0-40 steps long and needed by ~20% of the vertices, DESIGN.md
+// §5). The queue holds each query at most once and a block has at most 256 queries (one per path),
+// so a 256-entry ring cannot overflow.
+struct WalkPool {
+    LdsQueue q;
+    uint8_t* status;    // LDS [256] per owner column: 0 closest query, 1 shadow query, 2 done
+};
+enum : uint8_t { POOL_CLOSEST = 0, POOL_SHADOW = 1, POOL_DONE = 2 };
+constexpr int kPoolRefill = 8;  // refill only when at least this many lanes of the round are idle
+
+// Compact park of the walk pool (fits 3 blocks of 256 threads per CU, i.e. 3 waves/SIMD): no 1/d
+// (recomputed by make_inv when a query is loaded: the same bits), no NEE term (the owner keeps it in
+// registers), depth / pm / stk8 packed in one word. Doubles: ray o, d; box mn, mx; walk best t;
+// query t (closest hit so far / shadow distance). Ints: cur, depth | pm << 8 | stk8 << 16, path,
+// stk (2 words), order, lpos, lend, best, hit object, hit prim, gen slot, mesh, occluded.
+constexpr int kPark2D = 14, kPark2I = 14;
+enum : int { P2_T = 13, P2_HOBJ = 9, P2_HPRIM = 10, P2_OCC = 13 };
+RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
+    p.D(0) = r.wr.o.x; p.D(1) = r.wr.o.y; p.D(2) = r.wr.o.z;
+    p.D(3) = r.wr.d.x; p.D(4) = r.wr.d.y; p.D(5) = r.wr.d.z;
+    for (int k = 0; k < 3; ++k) { p.D(6 + k) = r.w.mn[k]; p.D(9 + k) = r.w.mx[k]; }
+    p.D(12) = r.w.bt;
+    p.D(13) = r.wt;
+    p.I(0) = r.w.cur;
+    p.I(1) = (int32_t)((uint32_t)r.w.depth | (r.w.pm << 8) | (r.w.stk8 << 16));
+    p.I(2) = (int32_t)r.w.path;
+    p.I(3) = (int32_t)(uint32_t)r.w.stk; p.I(4) = (int32_t)(uint32_t)(r.w.stk >> 32);
+    p.I(5) = (int32_t)r.w.order; p.I(6) = r.w.lpos; p.I(7) = r.w.lend; p.I(8) = r.w.best;
+    p.I(9) = r.hobj; p.I(10) = r.hprim; p.I(11) = r.g; p.I(12) = r.mi; p.I(13) = r.occluded;
+}
+RT_DEV void park2_load(const Park& p, WalkRegs& r) {
+    r.wr.o = v3(p.D(0), p.D(1), p.D(2));
+    r.wr.d = v3(p.D(3), p.D(4), p.D(5));
+    r.wi = make_inv(r.wr.d);
+    for (int k = 0; k < 3; ++k) { r.w.mn[k] = p.D(6 + k); r.w.mx[k] = p.D(9 + k); }
+    r.w.bt = p.D(12);
+    r.wt = p.D(13);
+    r.w.cur = p.I(0);
+    const uint32_t dps = (uint32_t)p.I(1);
+    r.w.depth = (int32_t)(dps & 0xFFu); r.w.pm = (dps >> 8) & 0xFFu; r.w.stk8 = dps >> 16;
+    r.w.path = (uint32_t)p.I(2);
+    r.w.stk = (uint64_t)(uint32_t)p.I(3) | ((uint64_t)(uint32_t)p.I(4) << 32);
+    r.w.order = (uint32_t)p.I(5); r.w.lpos = p.I(6); r.w.lend = p.I(7); r.w.best = p.I(8);
+    r.hobj = p.I(9); r.hprim = p.I(10); r.g = p.I(11); r.mi = p.I(12); r.occluded = p.I(13);
+}
+// A new pool query (see park_query).
+RT_DEV void park2_query(const Park& p, const Ray& r, double wt, int32_t hobj, int32_t hprim) {
+    p.D(0) = r.o.x; p.D(1) = r.o.y; p.D(2) = r.o.z;
+    p.D(3) = r.d.x; p.D(4) = r.d.y; p.D(5) = r.d.z;
+    p.D(13) = wt;
+    p.I(0) = -1;
+    p.I(9) = hobj; p.I(10) = hprim; p.I(11) = -1; p.I(13) = 0;
+}
+
+// One pool round: up to ksteps walk steps over queries taken from the pool; a lane whose query
+// finishes hands the result to its owner and, while steps remain, takes the next queued query
+// (refill: the round keeps its lanes full). Unfinished queries go back to the pool. All lanes call.
+template <class C>
+RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d, LdsInt* park_i, int need,
+                       int ksteps, const LdsTopI32* top) {
+    int32_t q = queue_take(wp.q, need);
+    if (!__any(q >= 0)) return false;
+    WalkRegs r;
+    bool closest = false;
+    auto col = [&](int32_t c) { return Park{park_d + c, park_i + c}; };
+    if (q >= 0) {
+        park2_load(col(q), r);
+        const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        closest = stq == POOL_CLOSEST;
+        if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
+    }
+    for (int k = 0; k < ksteps; ++k) {
+        RT_DBG_WAVE(10, lane_id_is0());
+        RT_DBG_WAVE(11, q >= 0);
+        if (q >= 0) {
+            bool fin = false;
+            if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
+                const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
+                fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, top);
+            } else {
+                double t;
+                int prim;
+                const int st = walk_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim, r.mi == sc.top_mesh ? top : nullptr);
+                if (st != WALK_RUN) {
+                    if (closest) {
+                        if (st == WALK_HIT) {
+                            HitRec h{r.wt, r.hobj, r.hprim};
+                            consider(h, t, tables(sc)->gen_idx[r.g], prim);
+                            r.wt = h.t;
+                            r.hobj = h.obj;
+                            r.hprim = h.prim;
+                        }
+                    } else {
+                        r.occluded = st == WALK_HIT && !(t + 0.001 >= r.wt);  // mutually_visible's ERR_MARGIN
+                        fin = r.occluded;
+                    }
+                    r.w.cur = -1;  // next step: the next mesh, if any
+                }
+            }
+            if (fin) {  // results for the owner's vertex phase, then the status word
+                const Park pq = col(q);
+                pq.D(P2_T) = r.wt;
+                pq.I(P2_HOBJ) = r.hobj;
+                pq.I(P2_HPRIM) = r.hprim;
+                pq.I(P2_OCC) = r.occluded;
+                __hip_atomic_store(&wp.status[q], (uint8_t)POOL_DONE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                q = -1;
+            }
+        }
+        if (k + 1 < ksteps && __popcll(__ballot(q < 0)) >= kPoolRefill) {
+            const int32_t q2 = queue_take_each(wp.q, q < 0);
+            if (q2 >= 0) {
+                q = q2;
+                park2_load(col(q), r);
+                const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                closest = stq == POOL_CLOSEST;
+                if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
+            }
+        }
+    }
+    if (q >= 0) park2_store(col(q), r);
+    queue_put(wp.q, q >= 0, q);
+    return true;
+}
+
+// Two-queue walk pool (P = 2): a walk alternates between triangle work (its open leaf's triangles,
+// leaf_tris) and node work (pop exhausted levels, pick the next child, open it or descend and mask its
+// children: walk_node; also a walk's start), and the two cost differently (a leaf step tests 2
+// triangles, a descent evaluates the 9 planes of octant_mask). With one queue a wave's 64 walks need
+// both kinds in every step and the wave pays for both with part of its lanes idle. Here each query
+// sits in the queue of the work it needs next (qt: triangles, qn: nodes); a wave takes a batch from
+// one queue and runs only that kind of step, so its lanes run the same code. A walk whose next work
+// changes kind is parked and moved to the other queue, its lane refilled from the round's queue.
+// Same steps, same order within each walk: same results as the one-queue pool (tested).
+struct WalkPool2 {
+    LdsQueue qt, qn;    // 256-entry rings: each query is in at most one of them
+    uint8_t* status;    // as WalkPool
+};
+template <class C>
+RT_DEV bool pool2_round(const DevScene& sc, const WalkPool2& wp, LdsDouble* park_d, LdsInt* park_i, int need,
+                        int ksteps, const LdsTopI32* top) {
+    // serve the longer queue that has `need` entries (wave-uniform lengths)
+    const uint32_t lt = __builtin_amdgcn_readfirstlane(queue_len(wp.qt));
+    const uint32_t ln = __builtin_amdgcn_readfirstlane(queue_len(wp.qn));
+    bool tq = lt > ln;
+    int32_t q = queue_take(tq ? wp.qt : wp.qn, need);
+    if (!__any(q >= 0)) {
+        tq = !tq;
+        q = queue_take(tq ? wp.qt : wp.qn, need);
+        if (!__any(q >= 0)) return false;
+    }
+    const LdsQueue& Q = tq ? wp.qt : wp.qn;
+    const LdsQueue& O = tq ? wp.qn : wp.qt;
+    WalkRegs r;
+    bool closest = false;
+    auto col = [&](int32_t c) { return Park{park_d + c, park_i + c}; };
+    if (q >= 0) {
+        park2_load(col(q), r);
+        const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        closest = stq == POOL_CLOSEST;
+        if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
+    }
+    for (int k = 0; k < ksteps; ++k) {
+        RT_DBG_WAVE(10, lane_id_is0());
+        RT_DBG_WAVE(11, q >= 0);
+        bool fin = false, flip = false;
+        if (q >= 0) {
+            if (tq) {  // triangle work: up to kTrisPerStep triangles of the open leaf
+                double t;
+                int prim;
+                const int st = leaf_tris(sc, r.wr, r.w, &t, &prim);
+                if (st == WALK_HIT) {  // the first subtree with a hit: this mesh's result
+                    if (closest) {
+                        HitRec h{r.wt, r.hobj, r.hprim};
+                        consider(h, t, tables(sc)->gen_idx[r.g], prim);
+                        r.wt = h.t;
+                        r.hobj = h.obj;
+                        r.hprim = h.prim;
+                    } else {
+                        r.occluded = !(t + 0.001 >= r.wt);  // mutually_visible's ERR_MARGIN
+                        fin = r.occluded;
+                    }
+                    r.w.cur = -1;  // next: the next mesh, if any (node work)
+                }
+                flip = !fin && st != WALK_RUN;  // leaf done: node work next
+            } else {  // node work: a walk's start, or pop + pick (+ descend)
+                if (r.w.cur < 0) {
+                    const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
+                    fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, top);
+                } else if (walk_node(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, r.mi == sc.top_mesh ? top : nullptr) ==
+                           WALK_MISS) {
+                    r.w.cur = -1;  // this mesh is exhausted: the next one, if any
+                }
+                flip = !fin && r.w.cur >= 0 && r.w.lpos < r.w.lend;  // a leaf is open: triangle work next
+            }
+            if (fin) {  // results for the owner's vertex phase, then the status word
+                const Park pq = col(q);
+                pq.D(P2_T) = r.wt;
+                pq.I(P2_HOBJ) = r.hobj;
+                pq.I(P2_HPRIM) = r.hprim;
+                pq.I(P2_OCC) = r.occluded;
+                __hip_atomic_store(&wp.status[q], (uint8_t)POOL_DONE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                q = -1;
+            } else if (flip) {
+                park2_store(col(q), r);
+            }
+        }
+        queue_put(O, flip, q);  // the walks whose next work is the other kind
+        if (flip) q = -1;
+        if (k + 1 < ksteps && __popcll(__ballot(q < 0)) >= kPoolRefill) {
+            const int32_t q2 = queue_take_each(Q, q < 0);
+            if (q2 >= 0) {
+                q = q2;
+                park2_load(col(q), r);
+                const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                closest = stq == POOL_CLOSEST;
+                if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
+            }
+        }
+    }
+    if (q >= 0) park2_store(col(q), r);
+    queue_put(Q, q >= 0, q);
+    return true;
+}
+
+template <int F, int W, int P>
+__global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
+                                                               uint32_t* next_sub, long nsub, int ksteps, int wmin,
+                                                               int refill, int pool_min, int pool_vmin) {
+    using C = Cfg<F>;
+    static_assert(C::mesh && C::compact, "mesh megakernel needs the compact tables");
+    // object table in LDS, as in k_megakernel_f64 (2 blocks per CU: 2 x 78 KB of LDS)
+    DevScene sc = sc_g;
+#if RT_OPT_LDSOBJ
+    __shared__ DevObject s_objs[kMaxCompactObjects];
+    {
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(sc_g.objects);
+        uint64_t* dst = reinterpret_cast<uint64_t*>(s_objs);
+        const int nw = sc_g.n_objects * (int)(sizeof(DevObject) / 8);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+        sc.objects = s_objs;
+    }
+#endif
+    __shared__ double s_park_d[(P ? kPark2D : kParkD) * kParkThreads];
+    __shared__ int32_t s_park_i[(P ? kPark2I : kParkI) * kParkThreads];
+    const Park park{(LdsDouble*)s_park_d + threadIdx.x, (LdsInt*)s_park_i + threadIdx.x};
+    // P = 1: one walk queue (s_ring[0]); P = 2: the triangle (s_ring[1]) and node (s_ring[0]) queues
+    __shared__ int32_t s_ring[P == 2 ? 2 : 1][P ? 256 : 1];
+    __shared__ uint8_t s_status[P ? 256 : 1];
+    __shared__ uint32_t s_qhead[2], s_qtail[2];
+    WalkPool wp;
+    wp.q = LdsQueue{s_ring[0], s_qhead, s_qtail, 255u};
+    wp.status = s_status;
+    WalkPool2 wp2;
+    wp2.qt = LdsQueue{s_ring[P == 2 ? 1 : 0], s_qhead + 1, s_qtail + 1, 255u};
+    wp2.qn = wp.q;
+    wp2.status = s_status;
+    // pool: the top kTopDepth + 1 levels of the deepest mesh's octree in LDS (18.3 KB; the walks of
+    // every query of the block start there), scene_layout.h: top_slot
+    __shared__ int4 s_top[P ? kTopNodes * 2 : 1];
+    const LdsTopI32* top = nullptr;
+    if constexpr (P) {
+        for (int j = 0; j < (P == 2 ? 2 : 1); ++j) s_ring[j][threadIdx.x] = -1;
+        if (threadIdx.x < 2) { s_qhead[threadIdx.x] = 0; s_qtail[threadIdx.x] = 0; }
+        if (sc.top_mesh >= 0) {
+            const int4* src = reinterpret_cast<const int4*>(sc.top_kids + sc.meshes[sc.top_mesh].top_base);
+            for (int i = threadIdx.x; i < kTopNodes * 2; i += blockDim.x) s_top[i] = src[i];
+            top = (const LdsTopI32*)(LdsInt*)s_top;
+        }
+        __syncthreads();
+    }
+    // subpixel accumulator and camera-sample buffer in LDS, as in k_megakernel_f64
+    // (no camera-sample buffer in pool mode: its 10 KB of LDS are what a third block per CU needs)
+    __shared__ double s_acc[3 * 256], s_nbd[P ? 1 : 3 * 256];
+    __shared__ uint64_t s_nbr[P ? 1 : 2 * 256];
+    LdsDouble* acc_l = (LdsDouble*)s_acc + threadIdx.x;
+    LdsDouble* nbd = (LdsDouble*)s_nbd + (P ? 0 : threadIdx.x);
+    LdsU64* nbr = (LdsU64*)s_nbr + (P ? 0 : threadIdx.x);
+    if constexpr (P) refill = 0;
+    V3 pc = v3(0, 0, 0);  // pool: the pending shadow query's NEE term (the park has no room for it)
+    uint32_t nverts = 0;
+    // tickets: whole subpixels, then the split tail's chunks (unit_of), as in k_megakernel_f64
+    const long n_split = nsub - a.n_whole;
+    const long nunits = a.n_wunits + n_split * a.tail_cps;
+    int id, end, s;
+    const long t0 = wave_ticket(next_sub, true);
+    unit_of(a, t0, id, end, s);
+    bool active = t0 < nunits;
+    acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
+    PathState ps;
+    bool fresh = true;
+    bool nvalid = false;
+    int phase = PH_TRACE;
+    bool walking = false, cont = false;
+    RT_DBG_TINIT();
+    while (__any(active)) {
+        RT_DBG_WAVE(8, lane_id_is0());
+        RT_DBG_TSTART(t_it);
+        RT_DBG_TSTART(t_wk);
+        bool took = false;
+        if constexpr (P) {
+            // take queued queries (at least pool_min of them while this wave has paths to shade)
+            const int ready = __popcll(__ballot(active && !walking));
+            if constexpr (P == 2)
+                took = pool2_round<C>(sc, wp2, (LdsDouble*)s_park_d, (LdsInt*)s_park_i, ready ? pool_min : 1, ksteps, top);
+            else
+                took = pool_round<C>(sc, wp, (LdsDouble*)s_park_d, (LdsInt*)s_park_i, ready ? pool_min : 1, ksteps, top);
+            if (!took && !ready) {
+                __builtin_amdgcn_s_sleep(2);  // every path of this wave waits on walks other waves hold
+            }
+            if (walking && __hip_atomic_load(&s_status[threadIdx.x], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == POOL_DONE)
+                walking = false;
+        } else if (__any(walking)) {
+            if (walk_round<C>(sc, park, walking, phase == PH_WALK_CLOSEST, ksteps, wmin)) walking = false;
+        }
+        RT_DBG_TEND(1, t_wk);
+        RT_DBG_TSTART(t_vx);
+        bool done = false;
+        const bool was_walking = walking;
+        // pool: after a walk round, shade only once pool_vmin paths are ready (denser vertex phases)
+        const bool vphase = !P || !took || __popcll(__ballot(active && !walking)) >= pool_vmin;
+        RT_DBG_WAVE(9, vphase && active && !walking);
+        if (vphase && active && !walking) {
+            bool shade_now = false, sample_end = false, trace_now = true;
+            HitRec h;
+            if (phase == PH_WALK_SHADOW) {  // the shadow result, then (path going on) the next trace
+                if constexpr (P) {
+                    if (!park.I(P2_OCC)) ps.L = ps.L + pc;
+                } else {
+                    if (!park.I(15)) ps.L = ps.L + v3(park.D(17), park.D(18), park.D(19));
+                }
+                phase = PH_TRACE;
+                sample_end = !cont;
+                trace_now = cont;
+            } else if (phase == PH_WALK_CLOSEST) {
+                h = P ? HitRec{park.D(P2_T), park.I(P2_HOBJ), park.I(P2_HPRIM)} : HitRec{park.D(16), park.I(11), park.I(12)};
+                shade_now = true;
+                trace_now = false;
+            }
+            if (trace_now) {
+                if (fresh) {
+                    if (!P && nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[256], nbd[512]), nbr[0], nbr[256]}, ps);
+                    else begin_sample(sc, a, subpixel_of(a, id), s, ps);
+                    nvalid = false;
+                    fresh = false;
+                }
+                const RayInv wi = make_inv(ps.ray.d);
+                h = trace_analytic<C>(sc, ps.ray, wi);
+                if (mesh_candidate<C>(sc, ps.ray, wi, h.obj >= 0 ? h.t : INFINITY)) {
+                    if constexpr (P) park2_query(park, ps.ray, h.t, h.obj, h.prim);
+                    else park_query(park, ps.ray, wi, h.t, h.obj, h.prim);
+                    if constexpr (P) s_status[threadIdx.x] = POOL_CLOSEST;
+                    phase = PH_WALK_CLOSEST;
+                    walking = true;
+                } else {
+                    shade_now = true;
+                }
+            }
+            if (shade_now) {
+                nverts += h.obj >= 0;
+                ShadowDefer df;
+                df.pending = false;
+                cont = shade_vertex<C>(sc, a, ps, h, &df);
+                phase = PH_TRACE;
+                if (df.pending) {  // shade_vertex found a mesh that could block the shadow ray
+                    const Ray sr{df.o, df.d};
+                    if constexpr (P) {
+                        park2_query(park, sr, df.dist, -1, -1);
+                        pc = df.c;
+                    } else {
+                        park_query(park, sr, make_inv(sr.d), df.dist, -1, -1);
+                        park.D(17) = df.c.x;
+                        park.D(18) = df.c.y;
+                        park.D(19) = df.c.z;
+                    }
+                    if constexpr (P) s_status[threadIdx.x] = POOL_SHADOW;
+                    phase = PH_WALK_SHADOW;
+                    walking = true;
+                }
+                if (!walking) sample_end = !cont;
+            }
+            if (sample_end) {
+                fresh = true;
+                if (id < a.n_whole) {
+                    V3 acc = v3(acc_l[0], acc_l[256], acc_l[512]);
+                    acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                    acc_l[0] = acc.x; acc_l[256] = acc.y; acc_l[512] = acc.z;
+                    if (++s == a.n_samples) {
+                        double* o = sub_buf + (size_t)id * 3;
+                        o[0] = acc.x;
+                        o[1] = acc.y;
+                        o[2] = acc.z;
+                        if (++id < end) {  // the next subpixel of the run, no ticket
+                            s = 0;
+                            acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
+                            nvalid = false;
+                        } else {
+                            done = true;
+                        }
+                    }
+                } else {  // split tail (k_tail_sum_f64)
+                    double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
+                    o[0] = ps.L.x;
+                    o[1] = ps.L.y;
+                    o[2] = ps.L.z;
+                    done = !unit_has_next(a, id, s);
+                    ++s;
+                }
+            }
+        }
+        if constexpr (P) queue_put(wp.q, walking && !was_walking, (int32_t)threadIdx.x);
+        RT_DBG_TEND(2, t_vx);
+        RT_DBG_TSTART(t_bk);
+        // camera-sample refill pass: lanes with a path in progress (walking or not) and a next sample
+        // in the same unit
+        const bool need = active && !fresh && !nvalid && unit_has_next(a, id, s);
+        if (refill > 0 && __popcll(__ballot(need)) >= refill) {
+            if (need) {
+                const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), s + 1);
+                nbd[0] = nb.d.x; nbd[256] = nb.d.y; nbd[512] = nb.d.z;
+                nbr[0] = nb.r0; nbr[256] = nb.r1;
+                nvalid = true;
+            }
+        }
+        bool stop = false;
+        if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+        const long nt = wave_ticket(next_sub, done && !stop);
+        if (__any(done)) flush_count(a.counters, nverts);  // keeps the 32-bit lane counts far from overflow
+        if (done) {
+            unit_of(a, nt, id, end, s);
+            active = !stop && nt < nunits;
+            acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
+            fresh = true;
+            nvalid = false;
+        }
+        RT_DBG_TEND(4, t_bk);
+        RT_DBG_TEND(0, t_it);
+    }
+    flush_count(a.counters, nverts);
+    RT_DBG_TFLUSH();
+}
+
+template <int F, int W, int P>
+static void launch_mm(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub, long nsub,
+                      int ksteps, int wmin, int refill, int pool_min, int pool_vmin, double* tail_buf, size_t tail_cap,
+                      hipStream_t st) {
+    const long blocks = resident_blocks(k_megakernel_mesh_f64<F, W, P>, (nsub + 255) / 256);
+    RenderArgs a = a_in;
+    plan_tail(a, nsub, blocks * 256, tail_buf, tail_cap);
+    hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W, P>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf,
+                       next_sub, nsub, ksteps, wmin, refill, pool_min, pool_vmin);
+    launch_tail_sum_f64(a, sub_buf, nsub - a.n_whole, st);
+}
+
+// Octree walks through the block's walk pool, 2 waves/SIMD (RT_MK_POOL=3: 3 waves/SIMD, 37 spilled
+// VGPRs, measured 6% slower; 0: each lane walks its own query, RT_MK_KSTEPS steps per iteration).
+hipError_t launch_megakernel_mesh_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
+                                      long nsub, int refill, int wmin, double* tail_buf, size_t tail_cap, hipStream_t st) {
+    static const int ksteps = std::max(1, env_int("RT_MK_KSTEPS", 4));
+    static const int pool = env_int("RT_MK_POOL", 1);
+    static const int pool_min = env_int("RT_MK_POOL_MIN", 32);
+    static const int pool_ksteps = std::max(1, env_int("RT_MK_POOL_KSTEPS", 6));
+    static const int pool_vmin = env_int("RT_MK_POOL_VMIN", 0);
+#define RT_MM_CASE(F)                                                                          \
+    case F:                                                                                    \
+        if (pool == 3) launch_mm<F, 3, 1>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
+        else if (pool == 2) launch_mm<F, 2, 2>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
+        else if (pool) launch_mm<F, 2, 1>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
+        else launch_mm<F, 2, 0>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, 0, 0, tail_buf, tail_cap, st); \
+        break;
+#define RT_MMB_CASE(F)                                                                         \
+    case F:                                                                                    \
+        launch_mm<F, 2, 0>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, 0, 0, tail_buf, tail_cap, st); \
+        break;
+    switch (a.features & 31) {
+        RT_MM_CASE(9) RT_MM_CASE(11) RT_MM_CASE(13) RT_MM_CASE(15)
+        RT_MMB_CASE(25) RT_MMB_CASE(27) RT_MMB_CASE(29) RT_MMB_CASE(31)  // nearest-triangle meshes: BVH walks
+        default: return hipErrorInvalidValue;
+    }
+#undef RT_MMB_CASE
+#undef RT_MM_CASE
+    return hipGetLastError();
+}
+
+#define RT_DIAG_TU_FN diag_read_mesh
+#include "diag_tu.h"
+
+}  // namespace rt

@@ -458,6 +458,7 @@ hipError_t Workspace::ensure_counters() {
 
 hipError_t Workspace::ensure_sub(size_t pixels) {
     if (sub_cap >= pixels) return hipSuccess;
+    if (in_flight && busy) (void)hipEventSynchronize(busy);  // a reused workspace: its last render is done with it
     if (sub_buf) (void)hipFree(sub_buf);
     sub_buf = nullptr;
     sub_cap = 0;
@@ -468,6 +469,7 @@ hipError_t Workspace::ensure_sub(size_t pixels) {
 
 hipError_t Workspace::ensure_tail(size_t bytes) {
     if (tail_cap >= bytes) return hipSuccess;
+    if (in_flight && busy) (void)hipEventSynchronize(busy);  // a reused workspace: its last render is done with it
     if (tail_buf) (void)hipFree(tail_buf);
     tail_buf = nullptr;
     tail_cap = 0;
@@ -487,6 +489,7 @@ hipError_t Workspace::ensure_slots(size_t n) {
         if (e != hipSuccess) return e;
     }
     if (slots >= n) return hipSuccess;
+    if (in_flight && busy) (void)hipEventSynchronize(busy);
     if (blob) (void)hipFree(blob);
     blob = nullptr;
     slots = 0;

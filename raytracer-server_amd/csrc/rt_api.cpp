@@ -228,7 +228,8 @@ void build_bvh(Packed& p, const rt::host::Mesh& m, int32_t tri_base) {
     if (n > 0) rec.build(0, n, 0);
 }
 
-void pack_scene(rt_scene* s) {
+// RT_OK, or RT_E_INVAL when the octree tables cannot encode the mesh (kid_leaf: leaf ids < 2^25).
+int pack_scene(rt_scene* s) {
     using namespace rt::host;
     Packed& p = s->packed;
     const Scene& sc = s->host;
@@ -344,6 +345,8 @@ void pack_scene(rt_scene* s) {
             p.up.push_back(int2{oc.parent[i] >= 0 ? oc.parent[i] + dm.node_base : -1, oc.slot[i]});
             for (int k = 0; k < 8; ++k) {
                 const int32_t c8 = oc.child[8 * i + k];
+                if (c8 >= 0 && oc.kind[c8] && leaf_of[c8] >= (1 << 25))  // kid_leaf's escape keeps leaf << 6 in an int32
+                    return fail(RT_E_INVAL, "mesh octree too large: leaf ids must stay below 2^25 (scene_layout.h kid_leaf)");
                 p.kids.push_back(c8 < 0 ? rt::kKidEmpty
                                  : oc.kind[c8] ? rt::kid_leaf(leaf_of[c8], p.leaves[leaf_of[c8]].x, p.leaves[leaf_of[c8]].y)
                                                : c8 + dm.node_base);
@@ -402,6 +405,7 @@ void pack_scene(rt_scene* s) {
         if (sc.light >= 0 && sc.light < (int)p.objects.size())
             for (int k = 0; k < 3; ++k) d.lef[k] = p.objects[sc.light].emitted[k] * d.kpi[k];
     }
+    return RT_OK;
 }
 
 // Groups objects for the compact trace (axis planes per axis, spheres, everything else).
@@ -645,24 +649,39 @@ int check_params(const rt_render_params* p) {
 
 // Per-render scratch (ticket counter, subpixel buffer, split-tail buffer, wavefront streams) comes
 // from a per-scene pool. rt_render_device returns before its kernels finish, so a pooled workspace
-// may still be in use on its stream: it is reused only by a render on the same stream (stream order
-// serialises the two) or once the event recorded after its last launch has completed; otherwise a
-// new workspace is made (concurrent renders on one scene each get their own, rt_ffi.h).
-std::unique_ptr<rt::Workspace> take_workspace(rt_scene* s, int device, hipStream_t st) {
+// may still be in use: an idle one (its completion event has fired) is taken first; else one last
+// used on the same stream, with a device-side wait on its completion event enqueued on `st` (so the
+// reuse is ordered even if the caller destroyed that stream and HIP handed its handle to a new one);
+// otherwise a new workspace is made (concurrent renders on one scene each get their own, rt_ffi.h).
+// A reused in-flight workspace never reallocates under its previous kernels: Workspace::ensure_*
+// wait for `busy` before freeing (wavefront_f64.hip).
+std::unique_ptr<rt::Workspace> take_workspace(rt_scene* s, int device, hipStream_t st, hipError_t* err) {
     std::lock_guard<std::mutex> lk(s->mu);
-    size_t pick = s->pool.size();
+    size_t idle = s->pool.size(), same = s->pool.size();
     for (size_t i = 0; i < s->pool.size(); ++i) {
         rt::Workspace& w = *s->pool[i];
         if (w.device != device) continue;
-        if (w.in_flight && w.last_stream == st) { pick = i; break; }  // stream-ordered after its last use
         if (!w.in_flight || hipEventQuery(w.busy) == hipSuccess) {
-            if (pick == s->pool.size()) pick = i;
+            idle = i;
+            break;
         }
+        if (w.last_stream == st && same == s->pool.size()) same = i;
     }
     (void)hipGetLastError();  // hipErrorNotReady from the queries is not an error
+    *err = hipSuccess;
+    const size_t pick = idle < s->pool.size() ? idle : same;
     if (pick < s->pool.size()) {
         std::unique_ptr<rt::Workspace> w = std::move(s->pool[pick]);
         s->pool.erase(s->pool.begin() + pick);
+        if (pick == idle) {
+            w->in_flight = false;
+        } else {
+            *err = hipStreamWaitEvent(st, w->busy, 0);
+            if (*err != hipSuccess) {  // keep it pooled; the caller fails the render
+                s->pool.push_back(std::move(w));
+                return nullptr;
+            }
+        }
         return w;
     }
     auto w = std::make_unique<rt::Workspace>();
@@ -685,9 +704,104 @@ void give_workspace(rt_scene* s, std::unique_ptr<rt::Workspace> w, hipStream_t s
     s->pool.push_back(std::move(w));
 }
 
-// Enqueue one render on `st` (device buffers). `cancel` is polled by the wavefront driver.
+// Device-visible mirror of a caller's cancel flag: a pinned, mapped word the megakernels poll
+// (RenderArgs::cancel) between subpixels. The caller's flag itself is never registered with HIP (it
+// may be shared by concurrent renders, or sit on memory HIP cannot pin): the host thread that waits
+// for the render copies it into the mirror (wait_stream), so its lifetime stays the caller's.
+struct CancelMirror {
+    int32_t* host = nullptr;
+    int32_t* dev = nullptr;
+    CancelMirror() = default;
+    CancelMirror(const CancelMirror&) = delete;
+    CancelMirror& operator=(const CancelMirror&) = delete;
+    ~CancelMirror() {
+        if (host) (void)hipHostFree(host);
+    }
+    hipError_t init() {
+        // coherent (fine-grained): hipHostMalloc's default is non-coherent memory the GPU may cache, so
+        // a host write could stay invisible to the polling kernel until the line is evicted
+        hipError_t e = hipHostMalloc((void**)&host, sizeof(int32_t),
+                                     hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
+        if (e != hipSuccess) {
+            host = nullptr;
+            return e;
+        }
+        *(volatile int32_t*)host = 0;
+        return hipHostGetDevicePointer((void**)&dev, host, 0);
+    }
+    void raise() {
+        if (host) __atomic_store_n(host, 1, __ATOMIC_RELEASE);
+    }
+};
+
+// Waits for everything enqueued on `st`, copying the caller's cancel flag into the mirror meanwhile.
+hipError_t wait_stream(hipStream_t st, const volatile int32_t* cancel, CancelMirror* mirror) {
+    if (!cancel || !mirror || !mirror->host) return hipStreamSynchronize(st);
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipErrorNotReady) return e;
+        if (*cancel) mirror->raise();
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
+// Statistics of an enqueued megakernel render, completed once its stream has drained (finish): the
+// render's HIP events and a pinned copy of the workspace's vertex counter (copied on the stream
+// before the workspace goes back to the pool). Nothing here synchronises, so callers can keep several
+// renders in flight (rt_render_multi) and still collect their stats.
+struct PendingStats {
+    rt_render_stats* out = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    unsigned long long* count = nullptr;  // pinned host word
+    int64_t samples = 0;
+    bool device_done = false;  // the wavefront path filled `out` itself
+    PendingStats() = default;
+    PendingStats(const PendingStats&) = delete;
+    PendingStats& operator=(const PendingStats&) = delete;
+    ~PendingStats() { release(); }
+    void release() {
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        if (count) (void)hipHostFree(count);
+        e0 = e1 = nullptr;
+        count = nullptr;
+    }
+    hipError_t init(rt_render_stats* o) {
+        out = o;
+        std::memset(out, 0, sizeof *out);
+        hipError_t e = hipEventCreate(&e0);
+        if (e == hipSuccess) e = hipEventCreate(&e1);
+        if (e == hipSuccess) e = hipHostMalloc((void**)&count, sizeof(unsigned long long), hipHostMallocDefault);
+        if (e == hipSuccess) *count = 0;
+        return e;
+    }
+    // after the render's stream has completed
+    int finish(std::string* err) {
+        if (!out) return RT_OK;
+        if (!device_done) {
+            float ms = 0.f;
+            const hipError_t e = hipEventElapsedTime(&ms, e0, e1);
+            if (e != hipSuccess) {
+                *err = std::string("stats: ") + hipGetErrorString(e);
+                return RT_E_HIP;
+            }
+            out->device_ms = ms;
+            out->kernel_ms[0] = ms;
+            out->kernel_launches[0] = 1;
+            out->vertices = (int64_t)*count;
+        }
+        out->samples = samples;
+        release();
+        return RT_OK;
+    }
+};
+
+// Enqueue one render on `st` (device buffers); returns without waiting for the device (except in
+// wavefront mode, whose host loop drives the bounces and polls host_cancel). dcancel: device view of
+// a cancel word the megakernels poll (CancelMirror::dev) or null; ps: stats to complete after the
+// stream drains (PendingStats::finish) or null.
 int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, double* d_sub, hipStream_t st,
-                   const volatile int32_t* cancel, rt_render_stats* stats) {
+                   const int32_t* dcancel, const volatile int32_t* host_cancel, PendingStats* ps) {
     int rc = check_params(p);
     if (rc != RT_OK) return rc;
     HIP_TRY(hipSetDevice(p->device));
@@ -710,7 +824,7 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
         a.features = (s->host.meshes.empty() ? 0 : 1) | (phong ? 2 : 0) | (a.mis ? 4 : 0) | (ds.compact ? 8 : 0);
         if ((p->flags & RT_FLAG_MESH_NEAREST) && !s->host.meshes.empty()) a.features |= 16;
         for (const auto& m : s->host.meshes) a.mesh_nodes = std::max(a.mesh_nodes, (int32_t)m.octree.size());
-        a.all_flat = !s->packed.meshes.empty() && s->packed.meshes.size() <= 2;  // render_flat_f64.h: kFlatMeshes
+        a.all_flat = !s->packed.meshes.empty() && s->packed.meshes.size() <= (size_t)rt::kFlatMeshes;
         for (const auto& dm : s->packed.meshes) a.all_flat &= dm.flat != 0;
     }
     a.seed = p->seed;
@@ -729,40 +843,31 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
     }
     if (!fp32 && (p->flags & RT_FLAG_MESH_NEAREST) && !(p->flags & RT_FLAG_MEGAKERNEL))
         return fail(RT_E_INVAL, "RT_FLAG_MESH_NEAREST needs RT_FLAG_MEGAKERNEL");
-    std::unique_ptr<rt::Workspace> ws = take_workspace(s, p->device, st);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (stats) {
-        std::memset(stats, 0, sizeof *stats);
-        HIP_TRY(hipEventCreate(&e0));
-        HIP_TRY(hipEventCreate(&e1));
-        HIP_TRY(hipEventRecord(e0, st));
+    const bool mk = fp32 || (p->flags & RT_FLAG_MEGAKERNEL);
+    if (ps) {
+        const hipError_t e = ps->init(ps->out);
+        if (e != hipSuccess) return fail(RT_E_HIP, std::string("stats: ") + hipGetErrorString(e));
+        ps->samples = (int64_t)p->tile_w * p->tile_h * 4 * (int64_t)a.n_samples;
+        HIP_TRY(hipEventRecord(ps->e0, st));
     }
+    hipError_t te;
+    std::unique_ptr<rt::Workspace> ws = take_workspace(s, p->device, st, &te);
+    if (!ws) return fail(RT_E_HIP, std::string("workspace: ") + hipGetErrorString(te));
     int out = RT_OK;
     std::string err;
-    if (fp32 || (p->flags & RT_FLAG_MEGAKERNEL)) {
+    if (mk) {
         const size_t npix = (size_t)p->tile_w * p->tile_h;
-        // device view of the caller's cancel flag: the megakernel polls it between subpixels
-        void* dcancel = nullptr;
-        bool registered = false;
-        if (cancel) {
-            hipError_t er = hipHostRegister((void*)cancel, sizeof(int32_t), hipHostRegisterMapped);
-            registered = er == hipSuccess;
-            if (er == hipSuccess || er == hipErrorHostMemoryAlreadyRegistered) {
-                if (hipHostGetDevicePointer(&dcancel, (void*)cancel, 0) != hipSuccess) dcancel = nullptr;
-            }
-            (void)hipGetLastError();
-        }
-        a.cancel = (const int32_t*)dcancel;
+        a.cancel = dcancel;
         hipError_t e = ws->ensure_counters();
         double* sub = d_sub;
         if (e == hipSuccess && !sub) {
             e = ws->ensure_sub(npix);
             sub = ws->sub_buf;
         }
-        if (e == hipSuccess && stats) e = hipMemsetAsync(ws->counters, 0, 8 * sizeof(unsigned long long), st);
+        if (e == hipSuccess && ps) e = hipMemsetAsync(ws->counters, 0, 8 * sizeof(unsigned long long), st);
         if (e == hipSuccess && a.n_samples <= 0) e = hipMemsetAsync(sub, 0, npix * 12 * sizeof(double), st);
         if (e == hipSuccess) {
-            a.counters = stats ? ws->counters : nullptr;
+            a.counters = ps ? ws->counters : nullptr;
             // split-tail scratch: up to one subpixel per resident lane, at most 1.5 GB
             const size_t per_sub = (size_t)std::max(0, a.n_samples) * 3 * sizeof(double);
             const size_t want = std::min<size_t>((size_t)3 << 29, per_sub * std::min<size_t>(npix * 4 / 2, (size_t)1 << 19));
@@ -778,35 +883,21 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
             }
         }
         if (e == hipSuccess) e = rt::launch_finalize_f64(a, sub, st);
+        if (e == hipSuccess && ps) e = hipEventRecord(ps->e1, st);
+        if (e == hipSuccess && ps) e = hipMemcpyAsync(ps->count, ws->counters, sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
         if (e != hipSuccess) { out = RT_E_HIP; err = std::string("megakernel: ") + hipGetErrorString(e); }
-        if (cancel) {
-            // the flag must stay registered until the kernel that polls it has finished
-            hipError_t es = hipStreamSynchronize(st);
-            if (es != hipSuccess && out == RT_OK) { out = RT_E_HIP; err = std::string("megakernel: ") + hipGetErrorString(es); }
-            if (registered) (void)hipHostUnregister((void*)cancel);
-            if (out == RT_OK && *cancel) out = RT_CANCELLED;
-        }
     } else {
-        out = rt::wavefront_render_f64(ds, a, *ws, st, cancel, stats, &err);
-    }
-    if (stats && out >= 0) {
-        hipError_t e = hipEventRecord(e1, st);
-        if (e == hipSuccess) e = hipEventSynchronize(e1);
-        float ms = 0.f;
-        if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
-        if (e == hipSuccess && (fp32 || (p->flags & RT_FLAG_MEGAKERNEL))) {
-            unsigned long long cnt[1] = {0};
-            e = hipMemcpy(cnt, ws->counters, sizeof cnt, hipMemcpyDeviceToHost);
-            stats->vertices = (int64_t)cnt[0];
-            stats->kernel_ms[0] = ms;
-            stats->kernel_launches[0] = 1;
+        out = rt::wavefront_render_f64(ds, a, *ws, st, host_cancel, ps ? ps->out : nullptr, &err);
+        if (ps && out >= 0) {
+            hipError_t e = hipEventRecord(ps->e1, st);
+            if (e == hipSuccess) e = hipEventSynchronize(ps->e1);
+            float ms = 0.f;
+            if (e == hipSuccess) e = hipEventElapsedTime(&ms, ps->e0, ps->e1);
+            if (e != hipSuccess && out == RT_OK) { out = RT_E_HIP; err = std::string("stats: ") + hipGetErrorString(e); }
+            ps->out->device_ms = ms;
+            ps->device_done = true;
         }
-        if (e != hipSuccess && out == RT_OK) { out = RT_E_HIP; err = std::string("stats: ") + hipGetErrorString(e); }
-        stats->device_ms = ms;
-        stats->samples = (int64_t)p->tile_w * p->tile_h * 4 * (int64_t)a.n_samples;
     }
-    if (e0) (void)hipEventDestroy(e0);
-    if (e1) (void)hipEventDestroy(e1);
     give_workspace(s, std::move(ws), st);
     if (out < 0) return fail(out, err);
     return out;
@@ -828,7 +919,8 @@ int rt_device_count(void) {
 static int finish_scene(rt::host::Scene&& sc, rt_scene** out) {
     auto s = std::make_unique<rt_scene>();
     s->host = std::move(sc);
-    pack_scene(s.get());
+    const int rc = pack_scene(s.get());
+    if (rc != RT_OK) return rc;
     *out = s.release();
     return RT_OK;
 }
@@ -919,8 +1011,17 @@ int rt_scene_mesh(const rt_scene* s, int32_t object, int64_t counts[4], double b
 int rt_render_device(const rt_scene* scene, const rt_render_params* params, void* d_rgb, void* d_sub, void* stream,
                      rt_render_stats* stats) {
     if (!scene || !d_rgb) return fail(RT_E_INVAL, "null argument");
-    return render_enqueue(const_cast<rt_scene*>(scene), params, (uint8_t*)d_rgb, (double*)d_sub, (hipStream_t)stream,
-                          nullptr, stats);
+    hipStream_t st = (hipStream_t)stream;
+    PendingStats ps;
+    ps.out = stats;
+    int rc = render_enqueue(const_cast<rt_scene*>(scene), params, (uint8_t*)d_rgb, (double*)d_sub, st, nullptr, nullptr,
+                            stats ? &ps : nullptr);
+    if (rc < 0 || !stats) return rc;
+    const hipError_t e = hipStreamSynchronize(st);  // stats: synchronous with respect to the stream (rt_ffi.h)
+    if (e != hipSuccess) return fail(RT_E_HIP, std::string("stats sync: ") + hipGetErrorString(e));
+    std::string err;
+    const int f = ps.finish(&err);
+    return f < 0 ? fail(f, err) : rc;
 }
 
 int rt_render(const rt_scene* scene, const rt_render_params* p, uint8_t* rgb_out, double* sub_out,
@@ -937,19 +1038,33 @@ int rt_render(const rt_scene* scene, const rt_render_params* p, uint8_t* rgb_out
     HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     hipError_t e = hipMalloc(&d_rgb, npix * 3);
     if (e == hipSuccess && sub_out) e = hipMalloc(&d_sub, npix * 12 * sizeof(double));
+    CancelMirror mirror;
+    if (e == hipSuccess && cancel) e = mirror.init();
     if (e != hipSuccess) {
         if (d_rgb) (void)hipFree(d_rgb);
+        if (d_sub) (void)hipFree(d_sub);
         (void)hipStreamDestroy(st);
-        return fail(RT_E_OOM, std::string("output buffers: ") + hipGetErrorString(e));
+        return fail(e == hipErrorOutOfMemory ? RT_E_OOM : RT_E_HIP, std::string("output buffers: ") + hipGetErrorString(e));
     }
     rt_render_stats local;
-    rc = render_enqueue(const_cast<rt_scene*>(scene), p, d_rgb, d_sub, st, cancel, stats ? stats : &local);
+    PendingStats ps;
+    ps.out = stats ? stats : &local;
+    rc = render_enqueue(const_cast<rt_scene*>(scene), p, d_rgb, d_sub, st, mirror.dev, cancel, &ps);
     std::string err = g_err;
     if (rc == RT_OK) {
-        e = hipMemcpyAsync(rgb_out, d_rgb, npix * 3, hipMemcpyDeviceToHost, st);
+        // wait for the render first (relaying the cancel flag), then copy back: a copy into the
+        // caller's pageable buffers would block inside hipMemcpyAsync until the kernel ends, with
+        // nobody relaying the flag
+        e = wait_stream(st, cancel, &mirror);
+        if (e == hipSuccess) e = hipMemcpyAsync(rgb_out, d_rgb, npix * 3, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess && sub_out) e = hipMemcpyAsync(sub_out, d_sub, npix * 12 * sizeof(double), hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) { rc = RT_E_HIP; err = std::string("readback: ") + hipGetErrorString(e); }
+        if (rc == RT_OK) {
+            const int f = ps.finish(&err);
+            if (f < 0) rc = f;
+        }
+        if (rc == RT_OK && cancel && *cancel) rc = RT_CANCELLED;
     } else {
         (void)hipStreamSynchronize(st);
     }
@@ -1001,6 +1116,14 @@ int rt_render_multi(const rt_scene* scene, const rt_render_params* p, const int3
     const auto t0 = std::chrono::steady_clock::now();
     rt_scene* s = const_cast<rt_scene*>(scene);
 
+    // one device-visible cancel word for every band of the call (the megakernels poll it between
+    // subpixels; each worker copies the caller's flag into it while it waits for a band)
+    CancelMirror mirror;
+    if (cancel) {
+        const hipError_t e = mirror.init();
+        if (e != hipSuccess) return fail(RT_E_HIP, std::string("rt_render_multi: cancel word: ") + hipGetErrorString(e));
+    }
+
     auto worker = [&](int32_t dev) {
         auto record = [&](int code, const std::string& m) {
             std::lock_guard<std::mutex> lk(err_mu);
@@ -1013,6 +1136,8 @@ int rt_render_multi(const rt_scene* scene, const rt_render_params* p, const int3
         uint8_t* d_rgb[kSlots] = {nullptr, nullptr};
         uint8_t* h_rgb[kSlots] = {nullptr, nullptr};
         int32_t pending[kSlots] = {-1, -1};
+        rt_render_stats bs[kSlots];
+        PendingStats ps[kSlots];
         const size_t band_bytes = (size_t)bmax * tw * 3;
         bool ok = true;
         for (int k = 0; k < kSlots && ok; ++k) {
@@ -1021,12 +1146,19 @@ int rt_render_multi(const rt_scene* scene, const rt_render_params* p, const int3
                  hipHostMalloc((void**)&h_rgb[k], band_bytes, hipHostMallocDefault) == hipSuccess;
         }
         if (!ok) record(RT_E_OOM, "rt_render_multi: band buffers");
-        // finishes band slot k: wait for its copy, put its rows into the caller's frame
+        // finishes band slot k: wait for its copy (relaying the cancel flag), collect its stats, put its
+        // rows into the caller's frame
         auto drain = [&](int k) {
             if (pending[k] < 0) return;
             const int32_t b = pending[k];
             pending[k] = -1;
-            if (hipStreamSynchronize(st[k]) != hipSuccess) { record(RT_E_HIP, "rt_render_multi: band sync"); return; }
+            if (wait_stream(st[k], cancel, &mirror) != hipSuccess) { record(RT_E_HIP, "rt_render_multi: band sync"); return; }
+            if (stats) {
+                std::string e;
+                if (ps[k].finish(&e) < 0) { record(RT_E_HIP, "rt_render_multi: " + e); return; }
+                samples += bs[k].samples;
+                vertices += bs[k].vertices;
+            }
             std::memcpy(rgb_out + (size_t)first[b] * tw * 3, h_rgb[k], (size_t)rows[b] * tw * 3);
             ++done;
         };
@@ -1039,10 +1171,9 @@ int rt_render_multi(const rt_scene* scene, const rt_render_params* p, const int3
             q.device = dev;
             q.y0 = (int32_t)(p->y0 + (int64_t)first[b] * step);
             q.tile_h = rows[b];
-            rt_render_stats bs;
-            const int r = render_enqueue(s, &q, d_rgb[slot], nullptr, st[slot], nullptr, stats ? &bs : nullptr);
+            ps[slot].out = &bs[slot];
+            const int r = render_enqueue(s, &q, d_rgb[slot], nullptr, st[slot], mirror.dev, cancel, stats ? &ps[slot] : nullptr);
             if (r < 0) { record(r, g_err); break; }
-            if (stats) { samples += bs.samples; vertices += bs.vertices; }
             if (hipMemcpyAsync(h_rgb[slot], d_rgb[slot], (size_t)rows[b] * tw * 3, hipMemcpyDeviceToHost, st[slot]) !=
                 hipSuccess) { record(RT_E_HIP, "rt_render_multi: band copy"); break; }
             pending[slot] = b;
@@ -1066,7 +1197,9 @@ int rt_render_multi(const rt_scene* scene, const rt_render_params* p, const int3
         stats->device_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         stats->kernel_launches[0] = nb;
     }
-    if (done.load() < nb) return RT_CANCELLED;  // only a cancel leaves bands unrendered without an error
+    // only a cancel leaves bands unrendered without an error; a band whose kernel saw the cancel word
+    // stopped handing out subpixels early
+    if (done.load() < nb || (cancel && *cancel)) return RT_CANCELLED;
     return RT_OK;
 }
 

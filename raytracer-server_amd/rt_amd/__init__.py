@@ -108,6 +108,8 @@ def _load():
     # diagnostics (include/rt_diag.h)
     if hasattr(L, "rt_selftest_arith"):  # absent from libraries built before it existed (A/B variants)
         L.rt_selftest_arith.argtypes = [ctypes.c_long, ctypes.c_ulonglong, P(ctypes.c_ulonglong)]
+    if hasattr(L, "rt_debug_qcheck"):
+        L.rt_debug_qcheck.argtypes = [P(ctypes.c_ulonglong)]
     if hasattr(L, "rt_debug_counters"):
         L.rt_debug_counters.argtypes = [P(ctypes.c_ulonglong)]
     if hasattr(L, "rt_debug_regions"):
@@ -347,10 +349,20 @@ class RenderJob:
 
 
 def selftest_arith(n=1 << 24, seed=0x5EED):
-    """Device check of the exact-division shortcuts: (reciprocal mismatches, quotient mismatches)."""
-    out = (ctypes.c_ulonglong * 2)()
+    """Device check of the exact-arithmetic shortcuts: (reciprocal, quotient, square-root mismatches)."""
+    out = (ctypes.c_ulonglong * 3)()
     _check(lib.rt_selftest_arith(n, seed, out))
-    return int(out[0]), int(out[1])
+    return int(out[0]), int(out[1]), int(out[2])
+
+
+def debug_qcheck():
+    """RT_QCHECK builds: LDS hand-off protocol violation counters since the last call (4 ints), or
+    None when the loaded library was built without the checks."""
+    out = (ctypes.c_ulonglong * 4)()
+    rc = lib.rt_debug_qcheck(out)
+    if rc < 0:
+        raise RtError(rc, "rt_debug_qcheck")
+    return None if rc == 1 else [int(v) for v in out]
 
 
 def device_count():

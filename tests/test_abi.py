@@ -26,9 +26,10 @@ def test_exports_every_declared_symbol(rt):
 def test_exports_diagnostics(rt):
     text = open(os.path.join(REPO, "include", "rt_diag.h")).read()
     names = re.findall(r"^int\s+(rt_[a-z_0-9]+)\s*\(", text, re.M)
-    assert names == ["rt_selftest_arith", "rt_debug_counters", "rt_debug_regions"]
+    assert names == ["rt_selftest_arith", "rt_debug_qcheck", "rt_debug_counters", "rt_debug_regions"]
     for n in names:
         assert hasattr(rt.lib, n), f"missing export {n}"
+    assert rt.debug_qcheck() is None  # the product library is built without the protocol checks
 
 
 def test_struct_layout_matches_header(rt, tmp_path):

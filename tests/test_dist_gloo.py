@@ -1,7 +1,8 @@
 """Multi-rank image tiling (bench.py's N > 1 path) rehearsed on CPU with the gloo backend.
 
 Each rank renders its rows (bench.partition: interleaved rows r, r+N, ... or contiguous stripes),
-the row sets are gathered to rank 0 exactly as bench.py does over RCCL, and the assembled frame
+the row sets are gathered to rank 0 exactly as bench.py does (a host gather over a gloo process group:
+no RCCL collective is on the data path), and the assembled frame
 (bench.assemble) must equal a single-rank render byte for byte:
 the RNG is keyed by the global pixel id, so the partition cannot change the image. The CPU oracle
 stands in for the GPU renderer here (test infrastructure only)."""

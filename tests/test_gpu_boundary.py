@@ -27,6 +27,7 @@ pytestmark = pytest.mark.gpu
 def _device_render(rt, torch, scene, w, h, spp, seed, stream, mis=False):
     p = rt.make_params(w, h, spp, seed, None, rt.FLAG_MEGAKERNEL | (rt.FLAG_MIS if mis else 0), 0, 1)
     buf = torch.zeros((h, w, 3), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the zero fill runs on the current stream: done before `stream` writes buf
     rt.render_device(scene, p, buf.data_ptr(), None, stream.cuda_stream)
     return buf
 
@@ -164,3 +165,39 @@ def test_ws_server_gpu_stop_rendering(rt, gpu_scenes, monkeypatch):
                                 rows=450 * 10, stop_after=10))  # 8192 spp: ~1.2 s per frame
     dt = time.time() - t0
     assert 10 <= len(msgs) < 450 * 10 and dt < 15.0, (len(msgs), dt)
+
+
+def test_concurrent_cancellable_renders_share_one_flag(rt, gpu_scenes):
+    """Two rt_render calls on two host threads share one cancel flag (the reference's per-job
+    AtomicBool, server.rs:226-251, viewed as an i32). The flag is never registered with HIP: each
+    render polls a pinned word of its own that its waiting thread copies the flag into, so one render
+    ending cannot unmap the flag under the other. Flag clear: both frames equal their serial renders.
+    Flag raised mid-render: both return RT_CANCELLED long before a full frame."""
+    s = gpu_scenes["cornell_box"]
+    w, h, spp = 256, 192, 64
+    ref = [rt.render(s, w, h, spp, SEED + k, megakernel=True)[0] for k in range(2)]
+    flag = ctypes.c_int32(0)
+    out = {}
+
+    def run(k, width, height, n):
+        out[k] = rt.render(s, width, height, n, SEED + k, megakernel=True, cancel=flag)
+
+    ts = [threading.Thread(target=run, args=(k, w, h, spp)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for k in range(2):
+        assert np.array_equal(out[k][0], ref[k]) and not out[k][2]["cancelled"], k
+    # 1920x1080 at 2048 spp: ~9 s per frame alone; the flag goes up after 0.3 s
+    timer = threading.Timer(0.3, lambda: setattr(flag, "value", 1))
+    t0 = time.time()
+    timer.start()
+    ts = [threading.Thread(target=run, args=(k, 1920, 1080, 2048)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    dt = time.time() - t0
+    timer.cancel()
+    assert out[0][2]["cancelled"] and out[1][2]["cancelled"] and dt < 3.0, (out[0][2]["cancelled"], out[1][2]["cancelled"], dt)

@@ -37,8 +37,9 @@ def _rays_for(name, n, rng):
 
 
 def test_exact_division_shortcuts(rt):
-    """rcp_rn / qdiv (path_f64.h) against IEEE division on the device: 2^24 operand pairs."""
-    assert rt.selftest_arith(1 << 24) == (0, 0)
+    """rcp_rn / qdiv / sqrt_rn (path_f64.h) against the IEEE operations on the device: 2^24 operands
+    each, spanning every exponent of the shortcuts' ranges (sqrt_rn: [2^-767, 2^1024))."""
+    assert rt.selftest_arith(1 << 24) == (0, 0, 0)
 
 
 @pytest.mark.parametrize("name", ["cornell_box", "cubes", "flying_unicorn"])
@@ -513,3 +514,24 @@ def test_root_leaf_mesh_with_scale_quirk(rt, oracle, tmp_path):
     for mk in (True, False):
         rgb_g, sub_g, _ = rt.render(sc, 64, 48, 16, SEED, megakernel=mk, want_sub=True)
         _assert_parity(rgb_g, sub_g, rgb_o, sub_o, f"root-leaf/{'mk' if mk else 'wf'}")
+
+
+def test_octree_first_hit_subtree_known_answer(rt, oracle, tmp_path):
+    """The hand-derived octree case of tests/octree_kat.py (geometry.rs:1245-1295) on
+    the device through rt_trace_rays: the walk returns the FARTHER triangle T_far, bit-identical to
+    the oracle; the nearest-triangle mode (RT_FLAG_MESH_NEAREST) returns T_near."""
+    import octree_kat as K
+
+    path = K.write_scene(tmp_path)
+    sc = rt.Scene.from_toml(path)
+    info = sc.info()
+    assert (info["nodes"], info["parents"], info["leaves"], info["refs"]) == (8, 3, 5, 14)
+    o, d = K.rays()
+    t_oct, t_near = K.expected_t(d)
+    orc = oracle.OracleScene(path)
+    for nearest, want, x0 in ((False, t_oct, K.T_FAR_X), (True, t_near, K.T_NEAR_X)):
+        t_g, id_g, p_g, n_g = sc.trace_ray(o, d, mesh_nearest=nearest)
+        t_o, id_o, p_o, n_o = (oracle.OracleScene(path, mesh_nearest=True) if nearest else orc).trace(o, d)
+        assert list(id_g) == [0, 0] and np.allclose(t_g, want, rtol=1e-12, atol=0)
+        assert abs(p_g[0, 0] - x0) < 1e-4
+        assert np.array_equal(t_g, t_o) and np.array_equal(p_g, p_o) and np.array_equal(n_g, n_o)

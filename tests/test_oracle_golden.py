@@ -105,3 +105,28 @@ def test_cubes_example_render_qualitative(oracle_scenes):
     gb = np.array(g["block_means"])
     assert np.corrcoef(blocks.ravel(), gb.ravel())[0, 1] >= 0.99
     assert np.median(np.abs(blocks - gb)) <= 5.0
+
+
+def test_octree_first_hit_subtree_known_answer(oracle, rt, tmp_path):
+    """SURVEY fact 6 pinned by a hand-derived case (tests/octree_kat.py: the build and the traversal
+    of geometry.rs:1149-1216 / 1245-1295 worked through on a 14-triangle mesh): the reference's
+    octree returns the FARTHER triangle T_far (t ~ 1.2003) because the root-octant-centre order
+    visits its leaf before T_near's (t ~ 0.4001); the nearest-triangle semantics return T_near."""
+    import octree_kat as K
+
+    path = K.write_scene(tmp_path)
+    orc = oracle.OracleScene(path)
+    st = orc.mesh_stats(0)
+    assert (st["nodes"], st["parents"], st["leaves"], st["refs"], st["n_tris"]) == (8, 3, 5, 14, 14)
+    assert np.array_equal(st["bbox"], [0, 0, 0, 4, 4, 4])
+    info = rt.Scene.from_toml(path).info()  # the product's host octree build (no device needed)
+    assert (info["nodes"], info["parents"], info["leaves"], info["refs"]) == (8, 3, 5, 14)
+    o, d = K.rays()
+    t_oct, t_near = K.expected_t(d)
+    t, obj, pos, n = orc.trace(o, d)
+    assert list(obj) == [0, 0]
+    assert np.allclose(t, t_oct, rtol=1e-12, atol=0)
+    assert abs(pos[0, 0] - K.T_FAR_X) < 1e-4 and t[0] > 1.2  # the farther triangle wins
+    t2, obj2, pos2, _ = oracle.OracleScene(path, mesh_nearest=True).trace(o, d)
+    assert list(obj2) == [0, 0] and np.allclose(t2, t_near, rtol=1e-12, atol=0)
+    assert abs(pos2[0, 0] - K.T_NEAR_X) < 1e-4

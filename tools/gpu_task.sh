@@ -7,7 +7,8 @@
 #   smoke            __graft_entry__.smoke()
 #   bench            python bench.py (headline line, cpu_baseline included)
 #   trace            rocprofv3 --kernel-trace --stats of `python bench.py --no-cpu-baseline`
-#   benchpmc         FETCH_SIZE / WRITE_SIZE passes over `bench.py --steps 1 --warmup 0` -> $OUT/pmc_traffic.json
+#   benchpmc         counter passes over `bench.py --steps 1 --warmup 0`: HBM bytes -> $OUT/pmc_traffic.json,
+#                    VALU mix + clock -> $OUT/pmc_valu.json (bench.py roofline.traffic / .compute)
 #   configs          tools/configs_bench.py (every BASELINE config, one GPU)
 #   pmc:SCENE:W:H:SPP[:mis]   counter passes on one megakernel render (tools/prof_render.py):
 #                    HBM traffic (FETCH_SIZE / WRITE_SIZE), L2 hit rate (TCC_HIT / TCC_MISS), clock
@@ -57,13 +58,22 @@ for task in "$@"; do
             python bench.py --no-cpu-baseline $BENCH_ARGS > "$OUT/trace.log" 2>&1 || fail trace "$OUT/trace.log"
         tail -1 "$OUT/trace.log" | cut -c1-300 ;;
     benchpmc)
-        # HBM traffic of the bench's own timed launch (roofline.traffic): separate FETCH / WRITE passes
+        # the bench command's own counters: HBM traffic (roofline.traffic; separate FETCH / WRITE passes)
+        # and the VALU instruction mix + clock (roofline.compute), each pass a run of its own
         B=(python bench.py --steps 1 --warmup 0 --no-cpu-baseline $BENCH_ARGS)
-        pmc_pass bench_fetch FETCH_SIZE -- "${B[@]}"
+        pmc_pass bench_fetch FETCH_SIZE GRBM_GUI_ACTIVE -- "${B[@]}"
         pmc_pass bench_write WRITE_SIZE -- "${B[@]}"
-        key=$(grep '^{"metric"' "$OUT/bench_fetch.log" | tail -1 | python -c "import json,sys;d=json.loads(sys.stdin.read());print(d['config']['workload'],d['config']['mode'])")
+        pmc_pass bench_sq1 $SQ1 -- "${B[@]}"
+        pmc_pass bench_sq2 $SQ2 -- "${B[@]}"
+        line=$(grep '^{"metric"' "$OUT/bench_fetch.log" | tail -1)
+        key=$(echo "$line" | python -c "import json,sys;d=json.loads(sys.stdin.read());print(d['config']['workload'],d['config']['mode'])")
+        # pmc_report.py reads the workload's sample / vertex counts and device time from a plain log
+        echo "$line" | python -c "import json,sys;d=json.loads(sys.stdin.read());c=d['config'];s=c['width']*c['height']*c['traced_spp'];print(f\"bench: samples {s}, vertices {c['vertices']}, {d['roofline']['kernel_ms']} ms device\")" > "$OUT/bench_plain.log"
         python tools/pmc_traffic.py "$OUT/bench_fetch/run_counter_collection.csv" "$OUT/bench_write/run_counter_collection.csv" \
-            "$key" --out "$OUT/pmc_traffic.json" || fail benchpmc ;;
+            "$key" --out "$OUT/pmc_traffic.json" || fail benchpmc
+        python tools/pmc_report.py "$OUT" bench k_megakernel --out "$OUT/pmc_bench.json" --valu-key "$key" \
+            --valu-out "$OUT/pmc_valu.json" > "$OUT/pmc_report.log" 2>&1 || fail "benchpmc report" "$OUT/pmc_report.log"
+        echo "benchpmc $key ok" ;;
     configs)
         timeout -k 10 900 python -u tools/configs_bench.py > "$OUT/configs.log" 2>&1 || fail configs "$OUT/configs.log"
         cat "$OUT/configs.log" ;;
