@@ -403,6 +403,55 @@ RT_DEV uint32_t root_order(const double d2[8]) {
     return order;
 }
 
+// root_order's result from the structure of the 8 root octant centres, a 2x2x2 grid: along axis k the
+// centres take two coordinates, with squared distances e0_k, e1_k from the origin (the very values
+// the radicand dv.x*dv.x + dv.y*dv.y + dv.z*dv.z sums), so up to rounding the radicand of an octant is
+// the sum of its near-half terms plus delta_k = |e1_k - e0_k| for every axis where it lies in the
+// far half. With the deltas sorted, da <= db <= dc, the octants in increasing radicand are: near,
+// +a, +b, then +a+b and +c (in the order of da + db vs dc), +a+c, +b+c, +a+b+c. The consecutive gaps
+// are da, db - da, dc - db and |dc - da - db|; when all exceed 2^-46 of the largest radicand (the
+// radicands carry two roundings, <= 2^-52 of it), the radicands in this order increase by more than
+// the 2^-50 that root_order requires to take its keys as distinct, so this IS root_order's result
+// (a strict order, no tie to break). Returns false otherwise (the caller runs root_order). ~70 VALU
+// instead of the radicands plus the 19-comparator network (~260).
+#ifndef RT_ROOT_GRID
+#define RT_ROOT_GRID 1  // A/B: 0 = always the sorting network
+#endif
+template <class MT>
+RT_DEV bool root_order_grid(const MT& m, const Ray& ray, uint32_t* order) {
+#if RT_ROOT_GRID
+    const double o[3] = {ray.o.x, ray.o.y, ray.o.z};
+    double dl[3], far[3];
+    uint32_t nb[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double lo = m.oct_center[0][k] - o[k], hi = m.oct_center[4 >> k][k] - o[k];  // octants 0 / 4, 2, 1
+        const double e0 = lo * lo, e1 = hi * hi;
+        nb[k] = e1 < e0 ? (4u >> k) : 0u;  // the nearer half's octant bit
+        dl[k] = fabs(e1 - e0);
+        far[k] = fmax(e0, e1);
+    }
+    // sort (delta, axis bit) ascending: a, b, c
+    double da = dl[0], db = dl[1], dc = dl[2];
+    uint32_t A = 4u, B = 2u, C = 1u;
+    if (db < da) { const double t = da; da = db; db = t; const uint32_t u = A; A = B; B = u; }
+    if (dc < db) { const double t = db; db = dc; dc = t; const uint32_t u = B; B = C; C = u; }
+    if (db < da) { const double t = da; da = db; db = t; const uint32_t u = A; A = B; B = u; }
+    const double sab = da + db;
+    const double gap = fmin(fmin(da, db - da), fmin(dc - db, fabs(dc - sab)));
+    const bool ok = gap > 0x1p-46 * (far[0] + far[1] + far[2]);
+    const uint32_t N = nb[0] | nb[1] | nb[2];
+    const bool abc = sab < dc;  // +a+b before +c
+    const uint32_t x3 = abc ? (N ^ A ^ B) : (N ^ C), x4 = abc ? (N ^ C) : (N ^ A ^ B);
+    *order = N | (N ^ A) << 4 | (N ^ B) << 8 | x3 << 12 | x4 << 16 | (N ^ A ^ C) << 20 | (N ^ B ^ C) << 24 |
+             (N ^ A ^ B ^ C) << 28;
+    return ok;
+#else
+    (void)m; (void)ray; (void)order;
+    return false;
+#endif
+}
+
 // BoundingBox::intersect(..).is_some() (geometry.rs:977-1036) for all 8 octants of the box
 // [mn, mx] at once; bit i = octant i (bit2 = x, bit1 = y, bit0 = z upper half, geometry.rs:1067-1099).
 // An octant's six faces lie on 9 planes (min / centre / max per axis), so each plane's crossing
@@ -521,25 +570,48 @@ struct OctWalk {
     int32_t lpos, lend;   // leaf triangle cursor
     int32_t best;         // nearest triangle so far in the current leaf (ltri index), -1 none
     double bt;
+    // Read-ahead of the next descent (the walk's dependent load chain: pick a child entry -> load that
+    // node's 8 child entries -> octant_mask -> pick ...): walk_enter takes the entry of the first child
+    // in visiting order from the node's child table it has in registers (nc), and when that child is
+    // a parent node below the LDS top levels, issues the load of ITS 8 child entries right away (pka,
+    // pkb), so the next step's pick needs no load and its walk_enter finds the entries arrived.
+    int32_t nc;           // the next pick's child entry at `cur`, or kNcNone (read it from the table)
+    int4 pka, pkb;        // node nc's child entries, loaded ahead (nc a parent below the top levels)
 };
+constexpr int32_t kNcNone = (int32_t)0x80000000;
 
 // Mask `cur`'s existing children whose boxes the ray hits, permuted to visiting order. (The child
 // table itself is not kept in registers: a pick reads its one entry again, an L2 hit.)
 // `top`: the LDS copy of this mesh's top levels (scene_layout.h: top_slot), or null; a node at depth
 // <= kTopDepth is then read from it (ds_read) instead of node_kids.
 typedef __attribute__((address_space(3))) int32_t LdsTopI32;
-RT_DEV void walk_enter(const DevScene& sc, const Ray& ray, const RayInv& inv, OctWalk& w,
-                       const LdsTopI32* top = nullptr) {
-    RT_DBG(2);
-    int4 ka, kb;
-    if (top && w.depth <= kTopDepth) {
-        const LdsTopI32* t = top + 8 * top_slot(w.depth, w.path);
+#ifndef RT_WALK_READAHEAD
+#define RT_WALK_READAHEAD 0  // A/B: OctWalk::nc / pka / pkb read-ahead of the next descent (1: measured 5% slower
+                             // on the unicorn, 141.4 vs 148.4 Msamples/s, profiles/r03_ab.log) or none (0)
+#endif
+// Loads node `node`'s child entries (from the LDS top levels when it sits there).
+RT_DEV void node_kids4(const DevScene& sc, int32_t node, int depth, uint32_t path, const LdsTopI32* top, int4& ka,
+                       int4& kb) {
+    if (top && depth <= kTopDepth) {
+        const LdsTopI32* t = top + 8 * top_slot(depth, path);
         ka = int4{t[0], t[1], t[2], t[3]};
         kb = int4{t[4], t[5], t[6], t[7]};
     } else {
-        const int4* k4 = reinterpret_cast<const int4*>(sc.node_kids + 8 * (size_t)w.cur);
+        const int4* k4 = reinterpret_cast<const int4*>(sc.node_kids + 8 * (size_t)node);
         ka = k4[0];
         kb = k4[1];
+    }
+}
+// `pre`: cur's child entries loaded ahead (OctWalk::pka / pkb), or null to load them here.
+RT_DEV void walk_enter(const DevScene& sc, const Ray& ray, const RayInv& inv, OctWalk& w,
+                       const LdsTopI32* top = nullptr, bool pre = false) {
+    RT_DBG(2);
+    int4 ka, kb;
+    if (pre) {
+        ka = w.pka;
+        kb = w.pkb;
+    } else {
+        node_kids4(sc, w.cur, w.depth, w.path, top, ka, kb);
     }
     const int32_t kid[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
     uint32_t m = octant_mask(w.mn, w.mx, ray, inv);
@@ -549,6 +621,33 @@ RT_DEV void walk_enter(const DevScene& sc, const Ray& ray, const RayInv& inv, Oc
 #pragma unroll
     for (int q = 0; q < 8; ++q) pm |= ((m >> ((w.order >> (4 * q)) & 0xF)) & 1u) << q;
     w.pm = pm;
+    w.nc = kNcNone;
+#if RT_WALK_READAHEAD
+    if (pm) {  // the first child in visiting order: the next pick's entry, and its own children ahead
+        const uint32_t oi = (w.order >> (4 * __builtin_ctz(pm))) & 0xF;
+        int32_t c = kid[0];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) c = oi == (uint32_t)i ? kid[i] : c;
+        w.nc = c;
+        if (c >= 0 && !(top && w.depth + 1 <= kTopDepth)) {
+            const int4* k4 = reinterpret_cast<const int4*>(sc.node_kids + 8 * (size_t)c);
+            w.pka = k4[0];
+            w.pkb = k4[1];
+        }
+    }
+#endif
+}
+// After a walk's state was reloaded (a parked walk): the read-ahead of node nc's entries again.
+RT_DEV void walk_reload_ahead(const DevScene& sc, OctWalk& w, const LdsTopI32* top = nullptr) {
+#if RT_WALK_READAHEAD
+    if (w.nc >= 0 && !(top && w.depth + 1 <= kTopDepth)) {
+        const int4* k4 = reinterpret_cast<const int4*>(sc.node_kids + 8 * (size_t)w.nc);
+        w.pka = k4[0];
+        w.pkb = k4[1];
+    }
+#else
+    (void)sc; (void)w; (void)top;
+#endif
 }
 
 // Starts a walk; false if the ray cannot produce a usable hit on this mesh (empty mesh, or the
@@ -567,6 +666,7 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
     w.stk = 0;
     w.stk8 = 0;
     w.pm = 0;
+    w.nc = kNcNone;
     if (m.root_leaf >= 0) {
         const int2 ls = sc.leaf_span[m.root_leaf];
         w.lpos = ls.x;
@@ -575,13 +675,20 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
         return true;
     }
     w.lpos = w.lend = 0;
-    double d2[8];
+    uint32_t order;
+    const bool grid = root_order_grid(m, ray, &order);
+    if (!wave_all(grid)) {
+        // a lane near a tie (or the A/B build without the grid form): the sorting network on the radicands
+        double d2[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        V3 dv = ld3(m.oct_center[i]) - ray.o;
-        d2[i] = dv.x * dv.x + dv.y * dv.y + dv.z * dv.z;  // mag()'s radicand, same operation order
+        for (int i = 0; i < 8; ++i) {
+            V3 dv = ld3(m.oct_center[i]) - ray.o;
+            d2[i] = dv.x * dv.x + dv.y * dv.y + dv.z * dv.z;  // mag()'s radicand, same operation order
+        }
+        const uint32_t o2 = root_order(d2);
+        if (!grid) order = o2;
     }
-    w.order = root_order(d2);
+    w.order = order;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         w.mn[k] = m.root_box[k];
@@ -660,8 +767,14 @@ RT_DEV int leaf_tris(const DevScene& sc, const Ray& ray, OctWalk& w, double* t, 
 // exhausted level, then picks the next child in visiting order and either opens it (a leaf: its
 // triangle range in w.lpos / w.lend) or descends into it and masks its children (walk_enter).
 // WALK_RUN, or WALK_MISS once the root is exhausted.
+// `anc` (with `top` only): this walk's LDS column of ancestor node ids at depths kTopDepth + 1 ..
+// kTopDepth + kAncLevels (stride 256 threads), written at each descent from those depths, so a pop
+// reads the ancestor it resumes at from LDS instead of following node_up (one dependent global load
+// per level popped); null: the node_up chain.
+constexpr int kAncLevels = 5;  // depths 4..8: the deepest parents sit at depth 8 (MAX_DEPTH 10, root depth 1)
 RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w,
-                     const LdsTopI32* top = nullptr) {
+                     const LdsTopI32* top = nullptr, LdsTopI32* anc = nullptr) {
+    RT_DBG_TSTART(t_pop);
     if (w.pm == 0) {  // `cur` exhausted: resume at the nearest ancestor with children left
         int lv = w.depth;
         uint32_t pm = 0;
@@ -669,17 +782,25 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
             --lv;
             pm = lv < 8 ? (uint32_t)(w.stk >> (8 * lv)) & 0xFFu : w.stk8;
         }
-        if (pm == 0) return WALK_MISS;  // the root is exhausted
+        if (pm == 0) {  // the root is exhausted
+            RT_DBG_TEND(13, t_pop);
+            return WALK_MISS;
+        }
         // the ancestor's node id through the parent links; not needed (and not loaded) when its
         // level is read from the LDS top levels (w.cur then keeps a stale id >= 0 until the next
         // descent sets it from a child entry)
         if (!(top && lv <= kTopDepth)) {
-            int32_t cur = w.cur;
-            for (int l = w.depth; l > lv; --l) cur = sc.node_up[cur].x;
-            w.cur = cur;
+            if (anc && top && lv <= kTopDepth + kAncLevels) {
+                w.cur = anc[(lv - kTopDepth - 1) * 256];
+            } else {
+                int32_t cur = w.cur;
+                for (int l = w.depth; l > lv; --l) cur = sc.node_up[cur].x;
+                w.cur = cur;
+            }
         }
         w.depth = lv;
         w.pm = pm;
+        w.nc = kNcNone;  // the ancestor's next entry is read from its table
         w.path &= (1u << (3 * lv)) - 1u;
         // the ancestor's box, rebuilt from the root along the path (the build's own arithmetic)
 #pragma unroll
@@ -696,11 +817,16 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
             }
         }
     }
+    RT_DBG_TEND(13, t_pop);
+    RT_DBG_TSTART(t_pick);
     const int q = __builtin_ctz(w.pm);
     w.pm &= w.pm - 1u;
     const uint32_t oi = (w.order >> (4 * q)) & 0xF;
-    const int32_t c = (top && w.depth <= kTopDepth) ? top[8 * top_slot(w.depth, w.path) + (int)oi]
-                                                    : sc.node_kids[8 * (size_t)w.cur + oi];
+    const bool ahead = RT_WALK_READAHEAD && w.nc != kNcNone;  // the first pick after walk_enter: its entry was read ahead
+    const int32_t c = ahead ? w.nc
+                            : (top && w.depth <= kTopDepth) ? top[8 * top_slot(w.depth, w.path) + (int)oi]
+                                                            : sc.node_kids[8 * (size_t)w.cur + oi];
+    w.nc = kNcNone;
     if (c <= -2) {  // open a leaf
         RT_DBG(3);
         const int32_t e = -2 - c;  // the leaf's range inline (kid_leaf), or its id behind the escape count
@@ -713,10 +839,12 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         w.lpos = first;
         w.lend = first + cnt;
         w.best = -1;
+        RT_DBG_TEND(14, t_pick);
         return WALK_RUN;
     }
     // descend: push the remaining mask of `cur`, take the octant's box
     const int lv = w.depth;
+    if (anc && top && lv > kTopDepth && lv <= kTopDepth + kAncLevels) anc[(lv - kTopDepth - 1) * 256] = w.cur;
     if (lv < 8) w.stk = (w.stk & ~(0xFFull << (8 * lv))) | ((uint64_t)w.pm << (8 * lv));
     else w.stk8 = w.pm;
     w.path |= oi << (3 * lv);
@@ -727,17 +855,19 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         const double cc = (w.mn[k] + w.mx[k]) / 2.0;
         if ((oi >> (2 - k)) & 1u) w.mn[k] = cc; else w.mx[k] = cc;
     }
-    walk_enter(sc, ray, inv, w, top);
+    walk_enter(sc, ray, inv, w, top, ahead && !(top && w.depth <= kTopDepth));
+    RT_DBG_TEND(14, t_pick);
     return WALK_RUN;
 }
 RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w, double* t,
-                     int* prim, const LdsTopI32* top = nullptr) {
+                     int* prim, const LdsTopI32* top = nullptr, LdsTopI32* anc = nullptr) {
     RT_DBG(5);
-    if (w.lpos < w.lend) {  // triangles of the open leaf
-        const int st = leaf_tris(sc, ray, w, t, prim);
-        if (st >= 0) return st;
-    }
-    const int st = walk_node(sc, m, ray, inv, w, top);
+    int st = -1;
+    RT_DBG_TSTART(t_lt);
+    if (w.lpos < w.lend) st = leaf_tris(sc, ray, w, t, prim);  // triangles of the open leaf
+    RT_DBG_TEND(12, t_lt);
+    if (st >= 0) return st;
+    st = walk_node(sc, m, ray, inv, w, top, anc);
 #if RT_WALK_OPEN_TEST
     if (st == WALK_RUN && w.lpos < w.lend) {  // a leaf was just opened: its first triangles in this step
         const int s2 = leaf_tris(sc, ray, w, t, prim);

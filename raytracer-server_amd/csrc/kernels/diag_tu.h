@@ -2,9 +2,11 @@
 // own copies of path_f64.h's g_dbg / g_dbg_region / g_dbg_time and megakernel_common.h's g_qcheck, so
 // each kernel TU includes this header once, at its end, with RT_DIAG_TU_FN naming its reader; the
 // rt_debug_* entry points (render_f64.hip) sum the readers of every TU.
-// Reader: adds this TU's counters to cnt16 / reg32 / tim16 / q4 and clears them; 0 or -1 (HIP error).
+// Reader: adds this TU's counters to cnt16 / reg32 / tim16 / q4 and clears them (a null output: that
+// set is left alone); 0 or -1 (HIP error).
 #define RT_DIAG_TAKE(sym, acc, n)                                                                         \
     do {                                                                                                  \
+        if (!(acc)) break;                                                                                \
         unsigned long long v_[n] = {0}, z_[n] = {0};                                                      \
         if (hipMemcpyFromSymbol(v_, HIP_SYMBOL(sym), sizeof(v_)) != hipSuccess ||                         \
             hipMemcpyToSymbol(HIP_SYMBOL(sym), z_, sizeof(z_)) != hipSuccess)                             \

@@ -389,11 +389,15 @@ extern "C" int rt_selftest_arith(long n, unsigned long long seed, unsigned long 
 #define RT_DIAG_TU_FN diag_read_main
 #include "diag_tu.h"
 
-// Diagnostic builds: the counters of every kernel code object, summed, then cleared (zeros otherwise).
+// Diagnostic builds: the counters of every kernel code object, summed, then cleared (zeros otherwise);
+// a null output leaves that set alone.
 static int diag_all(unsigned long long* cnt16, unsigned long long* reg32, unsigned long long* tim16, unsigned long long* q4) {
-    for (int i = 0; i < 16; ++i) cnt16[i] = tim16[i] = 0;
-    for (int i = 0; i < 32; ++i) reg32[i] = 0;
-    for (int i = 0; i < 4; ++i) q4[i] = 0;
+    for (int i = 0; i < 16; ++i) {
+        if (cnt16) cnt16[i] = 0;
+        if (tim16) tim16[i] = 0;
+    }
+    for (int i = 0; i < 32 && reg32; ++i) reg32[i] = 0;
+    for (int i = 0; i < 4 && q4; ++i) q4[i] = 0;
     if (diag_read_main(cnt16, reg32, tim16, q4) || diag_read_mesh(cnt16, reg32, tim16, q4) ||
         diag_read_flat(cnt16, reg32, tim16, q4))
         return -1;
@@ -404,24 +408,22 @@ static int diag_all(unsigned long long* cnt16, unsigned long long* reg32, unsign
 // returns 1 (and zeros) when the checks are not compiled in.
 extern "C" int rt_debug_qcheck(unsigned long long out[4]) {
 #if RT_QCHECK
-    unsigned long long c[16], r[32], t[16];
-    return diag_all(c, r, t, out);
+    return diag_all(nullptr, nullptr, nullptr, out);
 #else
     for (int i = 0; i < 4; ++i) out[i] = 0;
     return 1;
 #endif
 }
 
-// Diagnostic builds: read and clear the traversal counters (all zeros otherwise).
+// Diagnostic builds: read and clear the region counters and timers (all zeros otherwise).
 extern "C" int rt_debug_regions(unsigned long long out[64]) {
-    unsigned long long c[16], q[4];
     for (int i = 48; i < 64; ++i) out[i] = 0;
-    return diag_all(c, out, out + 32, q);
+    return diag_all(nullptr, out, out + 32, nullptr);
 }
 
+// Diagnostic builds: read and clear the traversal counters (all zeros otherwise).
 extern "C" int rt_debug_counters(unsigned long long out[16]) {
-    unsigned long long r[32], t[16], q[4];
-    return diag_all(out, r, t, q);
+    return diag_all(out, nullptr, nullptr, nullptr);
 }
 
 hipError_t launch_trace_f64(const DevScene& sc, long n, const double* o, const double* d, double* t, int32_t* obj,

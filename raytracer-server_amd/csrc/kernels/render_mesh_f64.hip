@@ -91,6 +91,7 @@ RT_DEV void park_load(const Park& p, WalkRegs& r) {
     r.w.stk = (uint64_t)(uint32_t)p.I(4) | ((uint64_t)(uint32_t)p.I(5) << 32); r.w.stk8 = (uint32_t)p.I(6);
     r.w.order = (uint32_t)p.I(7); r.w.lpos = p.I(8); r.w.lend = p.I(9); r.w.best = p.I(10);
     r.hobj = p.I(11); r.hprim = p.I(12); r.g = p.I(13); r.mi = p.I(14); r.occluded = p.I(15);
+    r.w.nc = kNcNone;  // the read-ahead is not parked here: the next pick reads its entry
 }
 
 // Nearest-triangle mode (Cfg::bvh): the BVH walk parks cur / sp / best / bt in the octree walk's
@@ -275,7 +276,7 @@ constexpr int kPoolRefill = 8;  // refill only when at least this many lanes of 
 // registers), depth / pm / stk8 packed in one word. Doubles: ray o, d; box mn, mx; walk best t;
 // query t (closest hit so far / shadow distance). Ints: cur, depth | pm << 8 | stk8 << 16, path,
 // stk (2 words), order, lpos, lend, best, hit object, hit prim, gen slot, mesh, occluded.
-constexpr int kPark2D = 14, kPark2I = 14;
+constexpr int kPark2D = 14, kPark2I = RT_WALK_READAHEAD ? 15 : 14;
 enum : int { P2_T = 13, P2_HOBJ = 9, P2_HPRIM = 10, P2_OCC = 13 };
 RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
     p.D(0) = r.wr.o.x; p.D(1) = r.wr.o.y; p.D(2) = r.wr.o.z;
@@ -289,6 +290,9 @@ RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
     p.I(3) = (int32_t)(uint32_t)r.w.stk; p.I(4) = (int32_t)(uint32_t)(r.w.stk >> 32);
     p.I(5) = (int32_t)r.w.order; p.I(6) = r.w.lpos; p.I(7) = r.w.lend; p.I(8) = r.w.best;
     p.I(9) = r.hobj; p.I(10) = r.hprim; p.I(11) = r.g; p.I(12) = r.mi; p.I(13) = r.occluded;
+#if RT_WALK_READAHEAD
+    p.I(14) = r.w.nc;
+#endif
 }
 RT_DEV void park2_load(const Park& p, WalkRegs& r) {
     r.wr.o = v3(p.D(0), p.D(1), p.D(2));
@@ -304,6 +308,11 @@ RT_DEV void park2_load(const Park& p, WalkRegs& r) {
     r.w.stk = (uint64_t)(uint32_t)p.I(3) | ((uint64_t)(uint32_t)p.I(4) << 32);
     r.w.order = (uint32_t)p.I(5); r.w.lpos = p.I(6); r.w.lend = p.I(7); r.w.best = p.I(8);
     r.hobj = p.I(9); r.hprim = p.I(10); r.g = p.I(11); r.mi = p.I(12); r.occluded = p.I(13);
+#if RT_WALK_READAHEAD
+    r.w.nc = p.I(14);  // its child entries are loaded again by walk_reload_ahead
+#else
+    r.w.nc = kNcNone;
+#endif
 }
 // A new pool query (see park_query).
 RT_DEV void park2_query(const Park& p, const Ray& r, double wt, int32_t hobj, int32_t hprim) {
@@ -312,6 +321,9 @@ RT_DEV void park2_query(const Park& p, const Ray& r, double wt, int32_t hobj, in
     p.D(13) = wt;
     p.I(0) = -1;
     p.I(9) = hobj; p.I(10) = hprim; p.I(11) = -1; p.I(13) = 0;
+#if RT_WALK_READAHEAD
+    p.I(14) = kNcNone;
+#endif
 }
 
 // One pool round: up to ksteps walk steps over queries taken from the pool; a lane whose query
@@ -320,29 +332,38 @@ RT_DEV void park2_query(const Park& p, const Ray& r, double wt, int32_t hobj, in
 template <class C>
 RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d, LdsInt* park_i, int need,
                        int ksteps, const LdsTopI32* top) {
+    RT_DBG_TSTART(t_tk);
     int32_t q = queue_take(wp.q, need);
-    if (!__any(q >= 0)) return false;
+    if (!__any(q >= 0)) {
+        RT_DBG_TEND(3, t_tk);
+        return false;
+    }
     WalkRegs r;
     bool closest = false;
     auto col = [&](int32_t c) { return Park{park_d + c, park_i + c}; };
     if (q >= 0) {
         park2_load(col(q), r);
+        if (r.w.cur >= 0) walk_reload_ahead(sc, r.w, r.mi == sc.top_mesh ? top : nullptr);
         const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         closest = stq == POOL_CLOSEST;
         if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
     }
+    RT_DBG_TEND(3, t_tk);
     for (int k = 0; k < ksteps; ++k) {
         RT_DBG_WAVE(10, lane_id_is0());
         RT_DBG_WAVE(11, q >= 0);
         if (q >= 0) {
             bool fin = false;
             if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
+                RT_DBG_TSTART(t_bg);
                 const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
                 fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, top);
+                RT_DBG_TEND(15, t_bg);
             } else {
                 double t;
                 int prim;
-                const int st = walk_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim, r.mi == sc.top_mesh ? top : nullptr);
+                const int st = walk_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim, r.mi == sc.top_mesh ? top : nullptr,
+                                         (LdsInt*)park_i + kPark2I * kParkThreads + q);
                 if (st != WALK_RUN) {
                     if (closest) {
                         if (st == WALK_HIT) {
@@ -374,14 +395,17 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
             if (q2 >= 0) {
                 q = q2;
                 park2_load(col(q), r);
+        if (r.w.cur >= 0) walk_reload_ahead(sc, r.w, r.mi == sc.top_mesh ? top : nullptr);
                 const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 closest = stq == POOL_CLOSEST;
                 if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
             }
         }
     }
+    RT_DBG_TSTART(t_pt);
     if (q >= 0) park2_store(col(q), r);
     queue_put(wp.q, q >= 0, q);
+    RT_DBG_TEND(5, t_pt);
     return true;
 }
 
@@ -418,6 +442,7 @@ RT_DEV bool pool2_round(const DevScene& sc, const WalkPool2& wp, LdsDouble* park
     auto col = [&](int32_t c) { return Park{park_d + c, park_i + c}; };
     if (q >= 0) {
         park2_load(col(q), r);
+        if (r.w.cur >= 0) walk_reload_ahead(sc, r.w, r.mi == sc.top_mesh ? top : nullptr);
         const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         closest = stq == POOL_CLOSEST;
         if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
@@ -449,7 +474,8 @@ RT_DEV bool pool2_round(const DevScene& sc, const WalkPool2& wp, LdsDouble* park
                 if (r.w.cur < 0) {
                     const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
                     fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, top);
-                } else if (walk_node(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, r.mi == sc.top_mesh ? top : nullptr) ==
+                } else if (walk_node(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, r.mi == sc.top_mesh ? top : nullptr,
+                                     (LdsInt*)park_i + kPark2I * kParkThreads + q) ==
                            WALK_MISS) {
                     r.w.cur = -1;  // this mesh is exhausted: the next one, if any
                 }
@@ -474,6 +500,7 @@ RT_DEV bool pool2_round(const DevScene& sc, const WalkPool2& wp, LdsDouble* park
             if (q2 >= 0) {
                 q = q2;
                 park2_load(col(q), r);
+        if (r.w.cur >= 0) walk_reload_ahead(sc, r.w, r.mi == sc.top_mesh ? top : nullptr);
                 const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 closest = stq == POOL_CLOSEST;
                 if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
@@ -505,7 +532,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     }
 #endif
     __shared__ double s_park_d[(P ? kPark2D : kParkD) * kParkThreads];
-    __shared__ int32_t s_park_i[(P ? kPark2I : kParkI) * kParkThreads];
+    __shared__ int32_t s_park_i[(P ? kPark2I + kAncLevels : kParkI) * kParkThreads];  // pool: + ancestor ids (walk_node)
     const Park park{(LdsDouble*)s_park_d + threadIdx.x, (LdsInt*)s_park_i + threadIdx.x};
     // P = 1: one walk queue (s_ring[0]); P = 2: the triangle (s_ring[1]) and node (s_ring[0]) queues
     __shared__ int32_t s_ring[P == 2 ? 2 : 1][P ? 256 : 1];
@@ -607,9 +634,12 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                     nvalid = false;
                     fresh = false;
                 }
+                RT_DBG_TSTART(t_ta);
                 const RayInv wi = make_inv(ps.ray.d);
                 h = trace_analytic<C>(sc, ps.ray, wi);
-                if (mesh_candidate<C>(sc, ps.ray, wi, h.obj >= 0 ? h.t : INFINITY)) {
+                const bool cand = mesh_candidate<C>(sc, ps.ray, wi, h.obj >= 0 ? h.t : INFINITY);
+                RT_DBG_TEND(6, t_ta);
+                if (cand) {
                     if constexpr (P) park2_query(park, ps.ray, h.t, h.obj, h.prim);
                     else park_query(park, ps.ray, wi, h.t, h.obj, h.prim);
                     if constexpr (P) s_status[threadIdx.x] = POOL_CLOSEST;
@@ -623,7 +653,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                 nverts += h.obj >= 0;
                 ShadowDefer df;
                 df.pending = false;
+                RT_DBG_TSTART(t_sv);
                 cont = shade_vertex<C>(sc, a, ps, h, &df);
+                RT_DBG_TEND(8, t_sv);
                 phase = PH_TRACE;
                 if (df.pending) {  // shade_vertex found a mesh that could block the shadow ray
                     const Ray sr{df.o, df.d};

@@ -258,3 +258,76 @@ def test_extra_assets_prep_matches_oracle(asset, rt, oracle, tmp_path):
     assert np.array_equal(m["indices"].astype(np.int64), idx_o.astype(np.int64))
     assert np.array_equal(m["kind"], kind_o) and np.array_equal(m["child"], child_o)
     assert np.array_equal(m["leaf_cnt"], cnt_o) and np.array_equal(m["refs"], refs_o)
+
+
+def test_root_order_grid_form_matches_insertion_sort():
+    """path_f64.h root_order_grid (the visiting order from the 2x2x2 structure of the root octant
+    centres, taken only when every consecutive radicand gap exceeds 2^-46 of the largest) restated
+    in f64 and checked against the reference's stable insertion sort by mag(centre - origin)
+    (geometry.rs:1248-1260) on random origins, origins near the root's mid-planes and near-equal
+    deltas: whenever the grid form claims a result, it is the reference's order."""
+    import math
+    import random
+
+    rnd = random.Random(11)
+    lo, hi = [11.657, -2.801, 56.176], [52.06, 59.347, 91.408]  # the unicorn's root box
+
+    def centres(lo, hi):
+        mid = [(a + b) / 2.0 for a, b in zip(lo, hi)]
+        cs = []
+        for i in range(8):
+            bmin = [mid[k] if (i >> (2 - k)) & 1 else lo[k] for k in range(3)]
+            bmax = [hi[k] if (i >> (2 - k)) & 1 else mid[k] for k in range(3)]
+            cs.append([(a + b) / 2.0 for a, b in zip(bmin, bmax)])
+        return cs
+
+    def reference(cs, o):
+        key = []
+        for c in cs:
+            dv = [c[0] - o[0], c[1] - o[1], c[2] - o[2]]
+            key.append(math.sqrt(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2]))
+        order = list(range(8))
+        for i in range(1, 8):
+            j = i
+            while j > 0 and key[order[j - 1]] > key[order[j]]:
+                order[j - 1], order[j] = order[j], order[j - 1]
+                j -= 1
+        return order
+
+    def grid(cs, o):
+        dl, far, nb = [], [], []
+        for k in range(3):
+            a, b = cs[0][k] - o[k], cs[4 >> k][k] - o[k]
+            e0, e1 = a * a, b * b
+            nb.append((4 >> k) if e1 < e0 else 0)
+            dl.append(abs(e1 - e0))
+            far.append(max(e0, e1))
+        ax = sorted(range(3), key=lambda k: (dl[k], k))  # the device's 3 compare-swaps are a stable sort
+        da, db, dc = (dl[k] for k in ax)
+        A, B, C = (4 >> k for k in ax)
+        sab = da + db
+        gap = min(min(da, db - da), min(dc - db, abs(dc - sab)))
+        ok = gap > 2.0 ** -46 * (far[0] + far[1] + far[2])
+        N = nb[0] | nb[1] | nb[2]
+        x3, x4 = ((N ^ A ^ B), (N ^ C)) if sab < dc else ((N ^ C), (N ^ A ^ B))
+        return ok, [N, N ^ A, N ^ B, x3, x4, N ^ A ^ C, N ^ B ^ C, N ^ A ^ B ^ C]
+
+    cs = centres(lo, hi)
+    mid = [(a + b) / 2.0 for a, b in zip(lo, hi)]
+    claimed = [0, 0, 0, 0]
+    for n in range(60000):
+        mode = n % 4
+        o = [rnd.uniform(lo[k] - 30, hi[k] + 30) for k in range(3)]
+        if mode == 1:  # on or next to a mid-plane
+            k = rnd.randrange(3)
+            o[k] = mid[k] + rnd.choice([0.0, 1e-13, -1e-13, 1e-9, 5e-16])
+        elif mode == 2:  # two deltas nearly equal: |o_x - mid_x| ~ |o_y - mid_y| (equal half-extents scaled)
+            t = rnd.uniform(0.1, 20)
+            o[0], o[1] = mid[0] + t, mid[1] + t * (hi[0] - lo[0]) / (hi[1] - lo[1]) * rnd.choice([1.0, 1 + 1e-14])
+        elif mode == 3:  # da + db ~ dc
+            o = [mid[k] + rnd.uniform(-3, 3) for k in range(3)]
+        ok, order = grid(cs, o)
+        if ok:
+            claimed[mode] += 1
+            assert order == reference(cs, o), (o, order, reference(cs, o))
+    assert claimed[0] > 0.999 * 15000 and claimed[3] > 0.99 * 15000  # random origins: the fast form almost always

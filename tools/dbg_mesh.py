@@ -31,6 +31,10 @@ print(f"  wave iterations {c[8]}: vertex-phase lanes/iteration {c[9] / it:.1f}, 
       f"walking lanes/step {c[11] / max(1, c[10]):.1f}")
 T = {0: "iteration", 1: "walk phase", 2: "vertex phase", 4: "refill + ticket", 7: "surface()", 9: "light_sample",
      10: "visible()", 11: "brdf_sample", 13: "trace: inv + planes", 14: "trace: spheres"}
+if scene != "cubes":  # the walk-pool kernel (render_mesh_f64.hip, path_f64.h walk_step)
+    T.update({3: "pool: take + park load", 5: "pool: park store + put", 6: "vertex: trace + mesh cull",
+              8: "vertex: shade_vertex", 12: "walk: leaf triangles", 13: "walk: pop", 14: "walk: pick + descend",
+              15: "walk: begin (root order)"})
 if os.environ.get("RT_MK_FLAT", "1") != "0" and scene == "cubes":  # render_flat_f64.hip phases
     T.update({1: "A camera + analytic", 2: "P mesh queries", 3: "C shadow results + shade + bookkeeping",
               6: "barrier waits"})
