@@ -772,6 +772,41 @@ RT_DEV int leaf_tris(const DevScene& sc, const Ray& ray, OctWalk& w, double* t, 
 // reads the ancestor it resumes at from LDS instead of following node_up (one dependent global load
 // per level popped); null: the node_up chain.
 constexpr int kAncLevels = 5;  // depths 4..8: the deepest parents sit at depth 8 (MAX_DEPTH 10, root depth 1)
+// Could any triangle of child `oi`'s subtree return tri_intersect == true for this ray? false only if
+// the ray (t >= 0) passes farther than the padding from the subtree's triangle bounds (scene_layout.h
+// kTightTop, dequantised against `cur`'s box w.mn / w.mx): the same conservative slab test as
+// near_box. Skipping such a child leaves the walk's result unchanged: the reference would descend,
+// test every triangle below it, find none, and go on with the next child in visiting order.
+#ifndef RT_WALK_TIGHT
+#define RT_WALK_TIGHT 1  // A/B: 0 = visit every child whose octant box the ray hits (the reference's walk)
+#endif
+RT_DEV bool kid_tight_hit(const DevScene& sc, const DevMesh& m, const OctWalk& w, const Ray& ray, const RayInv& inv,
+                          uint32_t oi, bool top_level) {
+    const uint2 q = top_level ? sc.top_tight[m.top_base + 8 * top_slot(w.depth, w.path) + (int)oi]
+                              : sc.node_tight[8 * (size_t)w.cur + oi];
+    const uint32_t ql[3] = {q.x & 0xFFu, (q.x >> 8) & 0xFFu, (q.x >> 16) & 0xFFu};
+    const uint32_t qh[3] = {q.x >> 24, q.y & 0xFFu, (q.y >> 8) & 0xFFu};
+    const double o[3] = {ray.o.x, ray.o.y, ray.o.z}, d[3] = {ray.d.x, ray.d.y, ray.d.z};
+    const double rc[3] = {inv.rx, inv.ry, inv.rz};
+    double t0 = 0.0, t1 = INFINITY;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double e = w.mx[k] - w.mn[k];
+        const double base = w.mn[k] - e, step = tight_step(e);
+        const double lo = ql[k] == 0u ? -INFINITY : fma((double)ql[k], step, base);
+        const double hi = qh[k] == (uint32_t)kTightTop ? INFINITY : fma((double)qh[k], step, base);
+        if (!(fabs(d[k]) >= 0x1p-900 && fabs(d[k]) <= 0x1p900)) {
+            if (!(fabs(d[k]) < 0x1p-900)) return true;  // NaN / huge: do not cull
+            if (o[k] < lo || o[k] > hi) return false;  // (nearly) parallel slab: origin must lie inside it
+            continue;
+        }
+        const double ta = (lo - o[k]) * rc[k], tb = (hi - o[k]) * rc[k];
+        const double tn = fmin(ta, tb), tf = fmax(ta, tb);
+        t0 = fmax(t0, tn - 1e-9 * fabs(tn));
+        t1 = fmin(t1, tf + 1e-9 * fabs(tf));
+    }
+    return t0 <= t1;
+}
 RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w,
                      const LdsTopI32* top = nullptr, LdsTopI32* anc = nullptr) {
     RT_DBG_TSTART(t_pop);
@@ -827,6 +862,13 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
                             : (top && w.depth <= kTopDepth) ? top[8 * top_slot(w.depth, w.path) + (int)oi]
                                                             : sc.node_kids[8 * (size_t)w.cur + oi];
     w.nc = kNcNone;
+#if RT_WALK_TIGHT
+    if (!kid_tight_hit(sc, m, w, ray, inv, oi, top && w.depth <= kTopDepth)) {  // no triangle below can be hit
+        RT_DBG(6);
+        RT_DBG_TEND(14, t_pick);
+        return WALK_RUN;
+    }
+#endif
     if (c <= -2) {  // open a leaf
         RT_DBG(3);
         const int32_t e = -2 - c;  // the leaf's range inline (kid_leaf), or its id behind the escape count

@@ -95,6 +95,17 @@ RT_LAYOUT_FN int top_slot(int depth, uint32_t path) {
     const int off = depth == 0 ? 0 : depth == 1 ? 1 : depth == 2 ? 9 : 73;  // (8^d - 1) / 7
     return off + (int)(path & ((1u << (3 * depth)) - 1u));
 }
+// Subtree triangle bounds ("tight boxes") of a node's children: node_tight[node][8] (top_tight[slot][8]
+// for the top levels, indexed like top_kids) holds, for child octant k, the bounding box of every
+// triangle in that child's subtree (leaf triangles' vertices, padded by DevMesh::cull_pad), rounded
+// outward to 8-bit codes over [mn - e, mx + e] per axis of the NODE's box (e = mx - mn): bound =
+// (mn - e) + q * e * 3/255, a low code 0 meaning -inf and a high code 255 +inf (triangles may reach far
+// outside their octant, geometry.rs:1038-1060 assigns any triangle that touches it). A ray that
+// passes farther than the padding from that box cannot get tri_intersect == true from any triangle of
+// the subtree, so the reference's walk would find nothing there: skipping the child changes no
+// result (Octree). x = lo x | lo y << 8 | lo z << 16 | hi x << 24, y = hi y | hi z << 8.
+constexpr int kTightTop = 255;
+RT_LAYOUT_FN double tight_step(double e) { return e * (3.0 / 255.0); }
 // node_up[node] = {parent node (-1 at the root), octant slot in the parent}
 // leaf_span[leaf] = {first entry of the leaf in ltri_id (ltris in RT_LTRI_INDEX=0 builds), count}
 
@@ -177,7 +188,9 @@ struct DevScene {
     const Tri32* btris32;
     const Compact32* ctab32;    // f32 compact tables (ok == 0: the generic object loop)
     const int32_t* top_kids;    // top-levels child tables of the meshes (DevMesh::top_base)
-    int32_t top_mesh;           // the mesh whose top levels the walk-pool kernel stages in LDS, -1 none
+    const uint2* node_tight;    // [node][8] children's subtree triangle bounds (kTightTop above)
+    const uint2* top_tight;     // the same for the top levels, indexed like top_kids
+    int32_t top_mesh;          // the mesh whose top levels the walk-pool kernel stages in LDS, -1 none
     int32_t top_pad;
     float off32;                // f32 mode: hit points are offset by off32 * n (scene-scaled epsilon)
     int32_t n_objects, light, n_meshes, compact;

@@ -58,7 +58,30 @@ struct Packed {
     std::vector<rt::DevTri> btris;
     std::vector<int32_t> btri_id;
     std::vector<int32_t> top_kids;  // [mesh tables][kTopNodes][8]: octree top levels by position (top_slot)
+    std::vector<uint2> tight;       // [node][8] children's subtree triangle bounds (scene_layout.h kTightTop)
+    std::vector<uint2> top_tight;   // the same, indexed like top_kids
 };
+
+// Quantized subtree bounds of a node's children (scene_layout.h, kTightTop): per child octant, the
+// vertex bounds of every triangle in its subtree padded by `pad`, rounded OUTWARD to 8-bit codes over
+// the parent box's [mn - e, mx + e] (one extra step each way, so device-side rounding of the
+// dequantised bounds cannot move them inward). bounds: [node] lo xyz, hi xyz of the subtree.
+uint2 quantize_tight(const rt::host::Box& parent, const double* b) {
+    const double pmn[3] = {parent.min.x, parent.min.y, parent.min.z}, pmx[3] = {parent.max.x, parent.max.y, parent.max.z};
+    uint32_t lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+        const double e = pmx[k] - pmn[k], base = pmn[k] - e, step = rt::tight_step(e);
+        if (!(step > 0.0) || !std::isfinite(step)) {  // degenerate axis: no bound along it
+            lo[k] = 0;
+            hi[k] = rt::kTightTop;
+            continue;
+        }
+        const double ql = std::floor((b[k] - base) / step) - 1.0, qh = std::ceil((b[3 + k] - base) / step) + 1.0;
+        lo[k] = ql >= 1.0 ? (uint32_t)std::min(ql, (double)(rt::kTightTop - 1)) : 0u;
+        hi[k] = qh <= (double)(rt::kTightTop - 1) ? (uint32_t)std::max(qh, 1.0) : (uint32_t)rt::kTightTop;
+    }
+    return uint2{lo[0] | lo[1] << 8 | lo[2] << 16 | hi[0] << 24, hi[1] | hi[2] << 8};
+}
 
 struct DeviceCopy {
     bool ready = false;
@@ -352,17 +375,69 @@ int pack_scene(rt_scene* s) {
                                                : c8 + dm.node_base);
             }
         }
+        {
+            // subtree triangle bounds (nodes are in DFS pre-order: children after their parent), then each
+            // parent's children quantised against the parent's box (scene_layout.h kTightTop)
+            std::vector<double> sb(oc.size() * 6);
+            auto tri_grow = [&](double* b, uint32_t t) {
+                const D3 v[3] = {m.vertices[m.indices[3 * t]], m.vertices[m.indices[3 * t + 1]], m.vertices[m.indices[3 * t + 2]]};
+                const rt::DevTri& dt = p.tris[dm.tri_base + t];
+                for (int k = 0; k < 3; ++k) {
+                    // the vertices, and a + ab / a + ac as tri_t's parametrisation sees them
+                    const double c[5] = {k == 0 ? v[0].x : k == 1 ? v[0].y : v[0].z, k == 0 ? v[1].x : k == 1 ? v[1].y : v[1].z,
+                                         k == 0 ? v[2].x : k == 1 ? v[2].y : v[2].z, dt.a[k] + dt.ab[k], dt.a[k] + dt.ac[k]};
+                    for (double x : c) {
+                        b[k] = std::fmin(b[k], x);
+                        b[3 + k] = std::fmax(b[3 + k], x);
+                    }
+                }
+            };
+            for (size_t j = oc.size(); j-- > 0;) {
+                double* b = &sb[6 * j];
+                for (int k = 0; k < 3; ++k) { b[k] = INFINITY; b[3 + k] = -INFINITY; }
+                if (oc.kind[j]) {
+                    for (int32_t r = 0; r < oc.leaf_cnt[j]; ++r) tri_grow(b, (uint32_t)oc.refs[oc.leaf_off[j] + r]);
+                } else {
+                    for (int k = 0; k < 8; ++k) {
+                        const int32_t c8 = oc.child[8 * j + k];
+                        if (c8 < 0) continue;
+                        for (int q = 0; q < 3; ++q) {
+                            b[q] = std::fmin(b[q], sb[6 * (size_t)c8 + q]);
+                            b[3 + q] = std::fmax(b[3 + q], sb[6 * (size_t)c8 + 3 + q]);
+                        }
+                    }
+                }
+            }
+            for (size_t j = 0; j < oc.size(); ++j) {
+                for (int k = 0; k < 8; ++k) {
+                    const int32_t c8 = oc.child[8 * j + k];
+                    if (c8 < 0) {
+                        p.tight.push_back(uint2{0u, 0u});
+                        continue;
+                    }
+                    double b[6];
+                    for (int q = 0; q < 3; ++q) {
+                        b[q] = sb[6 * (size_t)c8 + q] - dm.cull_pad;
+                        b[3 + q] = sb[6 * (size_t)c8 + 3 + q] + dm.cull_pad;
+                    }
+                    p.tight.push_back(quantize_tight(oc.box[j], b));
+                }
+            }
+        }
         // top levels (depths 0..kTopDepth) by position: what the walk-pool kernel stages in LDS
         dm.top_base = -1;
         if (oc.size() > 0 && !oc.kind[0]) {
             dm.top_base = (int32_t)p.top_kids.size();
             p.top_kids.resize(p.top_kids.size() + (size_t)rt::kTopNodes * 8, rt::kKidEmpty);
+            p.top_tight.resize(p.top_kids.size(), uint2{0u, 0u});
             int32_t* top = p.top_kids.data() + dm.top_base;
+            uint2* top_t = p.top_tight.data() + dm.top_base;
             std::function<void(int32_t, int, uint32_t)> fill = [&](int32_t node, int depth, uint32_t path) {
                 const int slot = rt::top_slot(depth, path);
                 for (int k = 0; k < 8; ++k) {
                     const int32_t e = p.kids[8 * (size_t)node + k];
                     top[8 * slot + k] = e;
+                    top_t[8 * slot + k] = p.tight[8 * (size_t)node + k];
                     if (e >= 0 && depth < rt::kTopDepth) fill(e, depth + 1, path | (uint32_t)k << (3 * depth));
                 }
             };
@@ -573,8 +648,10 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         put(blob, &o_obj32, obj32);
         put(blob, &o_bvh32, bvh32);
         put(blob, &o_tri32, tri32);
-        size_t o_top;
+        size_t o_top, o_tight, o_ttop;
         put(blob, &o_top, p.top_kids);
+        put(blob, &o_tight, p.tight);
+        put(blob, &o_ttop, p.top_tight);
         void* d = nullptr;
         HIP_TRY(hipMalloc(&d, blob.size()));
         hipError_t e = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice);
@@ -606,6 +683,8 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.compact = compact;
         // the walk-pool kernel stages the top levels of the largest octree in LDS (RT_MK_TOP=0: off, A/B)
         ds.top_kids = (const int32_t*)(b + o_top);
+        ds.node_tight = (const uint2*)(b + o_tight);
+        ds.top_tight = (const uint2*)(b + o_ttop);
         ds.top_mesh = -1;
         const char* top_env = std::getenv("RT_MK_TOP");
         if (!(top_env && std::atoi(top_env) == 0)) {

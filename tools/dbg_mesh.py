@@ -25,7 +25,7 @@ calls = max(1, c[0])
 it = max(1, c[8])
 print(f"{scene} {w}x{h}x{spp} {' '.join(k + '=' + v for k, v in os.environ.items() if k.startswith('RT_MK'))}: "
       f"device {st['device_ms']:.1f} ms, vertices {st['vertices']}, vertices/wave-iteration {st['vertices'] / it:.1f}")
-print(f"  mesh calls {c[0]}, past cull {c[1] / calls:.3f}; per call: nodes {c[2] / calls:.2f} leaves {c[3] / calls:.2f} "
+print(f"  mesh calls {c[0]}, past cull {c[1] / calls:.3f}; per call: nodes {c[2] / calls:.2f} leaves {c[3] / calls:.2f} culled picks {c[6] / calls:.2f} "
       f"tris {c[4] / calls:.2f} steps {c[5] / calls:.2f}")
 print(f"  wave iterations {c[8]}: vertex-phase lanes/iteration {c[9] / it:.1f}, walk steps/iteration {c[10] / it:.2f}, "
       f"walking lanes/step {c[11] / max(1, c[10]):.1f}")
