@@ -559,6 +559,9 @@ __shared__ unsigned long long s_dbg_time[4 * 16];
                          // slower while tri_t loaded triangles one by one, 0.5% once a step's triangles
                          // are preloaded (profiles/r02_ab.log): the copies stay the default
 #endif
+#ifndef RT_WALK_TIGHT
+#define RT_WALK_TIGHT 1  // A/B: 0 = visit every child whose octant box the ray hits (the reference's walk)
+#endif
 struct OctWalk {
     double mn[3], mx[3];  // box of `cur`
     int32_t cur, depth;
@@ -637,6 +640,17 @@ RT_DEV void walk_enter(const DevScene& sc, const Ray& ray, const RayInv& inv, Oc
     }
 #endif
 }
+// walk_enter for the slot walk: the node's existence mask comes with its parent's slot entry
+// (scene_layout.h KidSlot), so entering a node loads nothing.
+RT_DEV void walk_enter_mask(const Ray& ray, const RayInv& inv, OctWalk& w, uint32_t exist) {
+    RT_DBG(2);
+    const uint32_t m = octant_mask(w.mn, w.mx, ray, inv) & exist;
+    uint32_t pm = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) pm |= ((m >> ((w.order >> (4 * q)) & 0xF)) & 1u) << q;
+    w.pm = pm;  // (w.nc is not used by the slot walk; a store to it here let the compiler merge it with
+                // another field's store through a computed address, which kept the walk state in scratch)
+}
 // After a walk's state was reloaded (a parked walk): the read-ahead of node nc's entries again.
 RT_DEV void walk_reload_ahead(const DevScene& sc, OctWalk& w, const LdsTopI32* top = nullptr) {
 #if RT_WALK_READAHEAD
@@ -694,7 +708,12 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
         w.mn[k] = m.root_box[k];
         w.mx[k] = m.root_box[3 + k];
     }
+#if RT_WALK_TIGHT
+    (void)top;
+    walk_enter_mask(ray, inv, w, (uint32_t)m.root_exist);
+#else
     walk_enter(sc, ray, inv, w, top);
+#endif
     return true;
 }
 
@@ -772,40 +791,138 @@ RT_DEV int leaf_tris(const DevScene& sc, const Ray& ray, OctWalk& w, double* t, 
 // reads the ancestor it resumes at from LDS instead of following node_up (one dependent global load
 // per level popped); null: the node_up chain.
 constexpr int kAncLevels = 5;  // depths 4..8: the deepest parents sit at depth 8 (MAX_DEPTH 10, root depth 1)
-// Could any triangle of child `oi`'s subtree return tri_intersect == true for this ray? false only if
-// the ray (t >= 0) passes farther than the padding from the subtree's triangle bounds (scene_layout.h
-// kTightTop, dequantised against `cur`'s box w.mn / w.mx): the same conservative slab test as
-// near_box. Skipping such a child leaves the walk's result unchanged: the reference would descend,
-// test every triangle below it, find none, and go on with the next child in visiting order.
-#ifndef RT_WALK_TIGHT
-#define RT_WALK_TIGHT 1  // A/B: 0 = visit every child whose octant box the ray hits (the reference's walk)
-#endif
-RT_DEV bool kid_tight_hit(const DevScene& sc, const DevMesh& m, const OctWalk& w, const Ray& ray, const RayInv& inv,
-                          uint32_t oi, bool top_level) {
-    const uint2 q = top_level ? sc.top_tight[m.top_base + 8 * top_slot(w.depth, w.path) + (int)oi]
-                              : sc.node_tight[8 * (size_t)w.cur + oi];
-    const uint32_t ql[3] = {q.x & 0xFFu, (q.x >> 8) & 0xFFu, (q.x >> 16) & 0xFFu};
-    const uint32_t qh[3] = {q.x >> 24, q.y & 0xFFu, (q.y >> 8) & 0xFFu};
-    const double o[3] = {ray.o.x, ray.o.y, ray.o.z}, d[3] = {ray.d.x, ray.d.y, ray.d.z};
-    const double rc[3] = {inv.rx, inv.ry, inv.rz};
+// Could any triangle below the child of slot `ks` (scene_layout.h KidSlot) return tri_intersect ==
+// true for this ray? false only if the ray (t >= 0) passes farther than the padding from the child
+// subtree's triangle bounds: the same conservative slab test as near_box. Skipping such a child leaves
+// the walk's result unchanged: the reference would descend, test every triangle below it, find none,
+// and go on with the next child in visiting order.
+RT_DEV bool kid_tight_hit(const DevMesh& m, const int4& ks, const Ray& ray, const RayInv& inv) {
+    const double step = m.tight_step;
     double t0 = 0.0, t1 = INFINITY;
+    bool keep = true, force = false;
+    // one axis of near_box's slab test (branch-free: no private arrays, no early exits)
+    auto axis = [&](uint32_t ql, uint32_t qh, double base, double o, double d, double rc) {
+        const double lo = ql == 0u ? -INFINITY : fma((double)ql, step, base);
+        const double hi = qh == (uint32_t)kTightTop ? INFINITY : fma((double)qh, step, base);
+        const bool inr = fabs(d) >= 0x1p-900 && fabs(d) <= 0x1p900;
+        const bool tiny = fabs(d) < 0x1p-900;
+        force |= !inr && !tiny;                      // NaN / huge: do not cull
+        keep &= !tiny || (o >= lo && o <= hi);       // (nearly) parallel slab: origin must lie inside it
+        const double ta = (lo - o) * rc, tb = (hi - o) * rc;
+        const double tn = fmin(ta, tb), tf = fmax(ta, tb);
+        t0 = inr ? fmax(t0, tn - 1e-9 * fabs(tn)) : t0;
+        t1 = inr ? fmin(t1, tf + 1e-9 * fabs(tf)) : t1;
+    };
+    axis((uint32_t)ks.y & 0xFFFFu, (uint32_t)ks.z >> 16, m.tight_base[0], ray.o.x, ray.d.x, inv.rx);
+    axis((uint32_t)ks.y >> 16, (uint32_t)ks.w & 0xFFFFu, m.tight_base[1], ray.o.y, ray.d.y, inv.ry);
+    axis((uint32_t)ks.z & 0xFFFFu, (uint32_t)ks.w >> 16, m.tight_base[2], ray.o.z, ray.d.z, inv.rz);
+    return force || (keep && t0 <= t1);
+}
+// The slot of child octant oi of node `cur` (one 16-byte load: entry + bounds).
+RT_DEV int4 kid_slot(const DevScene& sc, int32_t cur, uint32_t oi) {
+    return *reinterpret_cast<const int4*>(sc.node_slot + 8 * (size_t)cur + oi);
+}
+// The node part of a walk step through the child slots (RT_WALK_TIGHT): as walk_node below, but a
+// pick reads the child's 16-byte slot (entry + subtree triangle bounds) and skips children whose
+// bounds the ray misses (up to two picks per step), and a descent takes the new node's existence
+// mask from the entry (no load). `anc` (or null: the node_up chain): this walk's LDS column of
+// ancestor node ids at depths 0 .. kSlotAncLevels - 1 (stride 256 threads), written at each descent,
+// so a pop reads the node it resumes at from LDS.
+constexpr int kSlotAncLevels = 9;
+#ifndef RT_SLOT_CULL
+#define RT_SLOT_CULL 1  // A/B: 0 = the slot walk without the subtree-bounds test
+#endif  // the deepest parents sit at depth 8 (MAX_DEPTH 10, root depth 1)
+RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w,
+                           LdsTopI32* anc = nullptr) {
+    RT_DBG_TSTART(t_pop);
+    if (w.pm == 0) {  // `cur` exhausted: resume at the nearest ancestor with children left
+        int lv = w.depth;
+        uint32_t pm = 0;
+        while (pm == 0 && lv > 0) {
+            --lv;
+            pm = lv < 8 ? (uint32_t)(w.stk >> (8 * lv)) & 0xFFu : w.stk8;
+        }
+        if (pm == 0) {  // the root is exhausted
+            RT_DBG_TEND(13, t_pop);
+            return WALK_MISS;
+        }
+        if (anc) {
+            w.cur = anc[lv * 256];
+        } else {
+            int32_t cur = w.cur;
+            for (int l = w.depth; l > lv; --l) cur = sc.node_up[cur].x;
+            w.cur = cur;
+        }
+        w.depth = lv;
+        w.pm = pm;
+        w.path &= (1u << (3 * lv)) - 1u;
+        // the ancestor's box, rebuilt from the root along the path (the build's own arithmetic)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            w.mn[k] = m.root_box[k];
+            w.mx[k] = m.root_box[3 + k];
+        }
+        for (int l = 0; l < lv; ++l) {
+            const uint32_t oi = (w.path >> (3 * l)) & 7u;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const double c = (w.mn[k] + w.mx[k]) / 2.0;
+                if ((oi >> (2 - k)) & 1u) w.mn[k] = c; else w.mx[k] = c;
+            }
+        }
+    }
+    RT_DBG_TEND(13, t_pop);
+    RT_DBG_TSTART(t_pick);
+    // the next child in visiting order whose subtree's triangle bounds the ray comes near; up to two
+    // picks per step (a culled pick is as if the reference found nothing below that child)
+    int32_t c = kKidEmpty;
+    uint32_t oi = 0;
+    for (int tries = 0; tries < 2; ++tries) {
+        const int q = __builtin_ctz(w.pm);
+        w.pm &= w.pm - 1u;
+        oi = (w.order >> (4 * q)) & 0xF;
+        const int4 ks = kid_slot(sc, w.cur, oi);
+        if (!RT_SLOT_CULL || kid_tight_hit(m, ks, ray, inv)) {
+            c = ks.x;
+            break;
+        }
+        RT_DBG(6);
+        if (w.pm == 0 || tries == 1) {  // nothing picked in this step
+            RT_DBG_TEND(14, t_pick);
+            return WALK_RUN;
+        }
+    }
+    if (c <= -2) {  // open a leaf
+        RT_DBG(3);
+        const int32_t e = -2 - c;  // the leaf's range inline (kid_leaf), or its id behind the escape count
+        int32_t first = e >> 6, cnt = e & 63;
+        if (cnt == kKidCountEscape) {
+            const int2 ls = sc.leaf_span[first];
+            first = ls.x;
+            cnt = ls.y;
+        }
+        w.lpos = first;
+        w.lend = first + cnt;
+        w.best = -1;
+        RT_DBG_TEND(14, t_pick);
+        return WALK_RUN;
+    }
+    // descend: push the remaining mask of `cur`, take the octant's box
+    const int lv = w.depth;
+    if (anc) anc[lv * 256] = w.cur;
+    if (lv < 8) w.stk = (w.stk & ~(0xFFull << (8 * lv))) | ((uint64_t)w.pm << (8 * lv));
+    else w.stk8 = w.pm;
+    w.path |= oi << (3 * lv);
+    w.depth = lv + 1;
+    w.cur = slot_node(c);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const double e = w.mx[k] - w.mn[k];
-        const double base = w.mn[k] - e, step = tight_step(e);
-        const double lo = ql[k] == 0u ? -INFINITY : fma((double)ql[k], step, base);
-        const double hi = qh[k] == (uint32_t)kTightTop ? INFINITY : fma((double)qh[k], step, base);
-        if (!(fabs(d[k]) >= 0x1p-900 && fabs(d[k]) <= 0x1p900)) {
-            if (!(fabs(d[k]) < 0x1p-900)) return true;  // NaN / huge: do not cull
-            if (o[k] < lo || o[k] > hi) return false;  // (nearly) parallel slab: origin must lie inside it
-            continue;
-        }
-        const double ta = (lo - o[k]) * rc[k], tb = (hi - o[k]) * rc[k];
-        const double tn = fmin(ta, tb), tf = fmax(ta, tb);
-        t0 = fmax(t0, tn - 1e-9 * fabs(tn));
-        t1 = fmin(t1, tf + 1e-9 * fabs(tf));
+        const double cc = (w.mn[k] + w.mx[k]) / 2.0;
+        if ((oi >> (2 - k)) & 1u) w.mn[k] = cc; else w.mx[k] = cc;
     }
-    return t0 <= t1;
+    walk_enter_mask(ray, inv, w, slot_exist(c));
+    RT_DBG_TEND(14, t_pick);
+    return WALK_RUN;
 }
 RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w,
                      const LdsTopI32* top = nullptr, LdsTopI32* anc = nullptr) {
@@ -862,13 +979,6 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
                             : (top && w.depth <= kTopDepth) ? top[8 * top_slot(w.depth, w.path) + (int)oi]
                                                             : sc.node_kids[8 * (size_t)w.cur + oi];
     w.nc = kNcNone;
-#if RT_WALK_TIGHT
-    if (!kid_tight_hit(sc, m, w, ray, inv, oi, top && w.depth <= kTopDepth)) {  // no triangle below can be hit
-        RT_DBG(6);
-        RT_DBG_TEND(14, t_pick);
-        return WALK_RUN;
-    }
-#endif
     if (c <= -2) {  // open a leaf
         RT_DBG(3);
         const int32_t e = -2 - c;  // the leaf's range inline (kid_leaf), or its id behind the escape count
@@ -901,6 +1011,10 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
     RT_DBG_TEND(14, t_pick);
     return WALK_RUN;
 }
+// Slots = the slot walk (walk_node_slots, RT_WALK_TIGHT) or the node_kids walk (walk_node); both give
+// the reference's result. (The wavefront's persistent walk kernels use the node_kids walk: the slot
+// walk inlined there trips an AMDGPU backend error, "illegal VGPR to SGPR copy", in ROCm 7.2.)
+template <bool Slots = (RT_WALK_TIGHT != 0)>
 RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w, double* t,
                      int* prim, const LdsTopI32* top = nullptr, LdsTopI32* anc = nullptr) {
     RT_DBG(5);
@@ -909,7 +1023,8 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
     if (w.lpos < w.lend) st = leaf_tris(sc, ray, w, t, prim);  // triangles of the open leaf
     RT_DBG_TEND(12, t_lt);
     if (st >= 0) return st;
-    st = walk_node(sc, m, ray, inv, w, top, anc);
+    if constexpr (Slots) st = walk_node_slots(sc, m, ray, inv, w, anc);
+    else st = walk_node(sc, m, ray, inv, w, top, anc);
 #if RT_WALK_OPEN_TEST
     if (st == WALK_RUN && w.lpos < w.lend) {  // a leaf was just opened: its first triangles in this step
         const int s2 = leaf_tris(sc, ray, w, t, prim);

@@ -54,7 +54,9 @@ struct alignas(16) DevMesh {
     int32_t btri_base;        // first of this mesh's n_tris BVH-order triangles (DevScene::btris)
     int32_t top_base;         // this mesh's top-levels child table in DevScene::top_kids (kTopNodes x 8
                               // entries), or -1 (root leaf / empty octree)
-    int32_t pad1, pad2;
+    int32_t root_exist;       // the root's existence mask (KidSlot): the slot walk's first walk_enter
+    int32_t pad2;
+    double tight_base[3], tight_step;  // KidSlot bounds: base[k] + q * step (cull box min - E, 3 E / 65535)
     // Flat octree (the cubes): the root is a leaf, or a parent whose children are all leaves, with at
     // most kFlatMaxTris triangles and every leaf list in triangle order. flat_leaf[j / 4] byte j % 4 =
     // the leaves (octant bits; bit 0 for a root leaf) that hold triangle j; flat_kids = octants with a
@@ -95,17 +97,27 @@ RT_LAYOUT_FN int top_slot(int depth, uint32_t path) {
     const int off = depth == 0 ? 0 : depth == 1 ? 1 : depth == 2 ? 9 : 73;  // (8^d - 1) / 7
     return off + (int)(path & ((1u << (3 * depth)) - 1u));
 }
-// Subtree triangle bounds ("tight boxes") of a node's children: node_tight[node][8] (top_tight[slot][8]
-// for the top levels, indexed like top_kids) holds, for child octant k, the bounding box of every
-// triangle in that child's subtree (leaf triangles' vertices, padded by DevMesh::cull_pad), rounded
-// outward to 8-bit codes over [mn - e, mx + e] per axis of the NODE's box (e = mx - mn): bound =
-// (mn - e) + q * e * 3/255, a low code 0 meaning -inf and a high code 255 +inf (triangles may reach far
-// outside their octant, geometry.rs:1038-1060 assigns any triangle that touches it). A ray that
-// passes farther than the padding from that box cannot get tri_intersect == true from any triangle of
-// the subtree, so the reference's walk would find nothing there: skipping the child changes no
-// result (Octree). x = lo x | lo y << 8 | lo z << 16 | hi x << 24, y = hi y | hi z << 8.
-constexpr int kTightTop = 255;
-RT_LAYOUT_FN double tight_step(double e) { return e * (3.0 / 255.0); }
+// A walk's child pick reads one 16-byte slot: node_slot[node][8] = the child entry (as node_kids,
+// with the parent encoding below) and the child subtree's triangle
+// bounds ("tight box": the vertices of every triangle in the subtree's leaves, padded by
+// DevMesh::cull_pad), rounded OUTWARD to 16-bit codes over the mesh's range (DevMesh::tight_base /
+// tight_step: bound = base + q * step, one extra step each way; a low code 0 means -inf, a high code
+// 65535 +inf). Triangles may reach far outside their octant (geometry.rs:1038-1060 assigns any
+// triangle that touches it), so the bounds are not the octant box. A ray that passes farther than the
+// padding from them cannot get tri_intersect == true from any triangle below, so the reference's walk
+// would find nothing there: skipping the child changes no result (Octree).
+// A parent child's entry in a slot also carries that child's own existence mask (bit k: its octant k
+// holds a node), so entering it needs no load: entry = node id | mask << 23 (ids < 2^23); leaf and
+// empty entries as in node_kids.
+struct alignas(16) KidSlot {
+    int32_t kid;
+    uint16_t lo[3], hi[3];
+};
+constexpr int kTightTop = 65535;
+constexpr int32_t kSlotMaxNode = 1 << 23;
+RT_LAYOUT_FN int32_t slot_parent(int32_t node, uint32_t exist) { return node | (int32_t)(exist << 23); }
+RT_LAYOUT_FN int32_t slot_node(int32_t e) { return e & (kSlotMaxNode - 1); }
+RT_LAYOUT_FN uint32_t slot_exist(int32_t e) { return (uint32_t)e >> 23; }
 // node_up[node] = {parent node (-1 at the root), octant slot in the parent}
 // leaf_span[leaf] = {first entry of the leaf in ltri_id (ltris in RT_LTRI_INDEX=0 builds), count}
 
@@ -188,8 +200,7 @@ struct DevScene {
     const Tri32* btris32;
     const Compact32* ctab32;    // f32 compact tables (ok == 0: the generic object loop)
     const int32_t* top_kids;    // top-levels child tables of the meshes (DevMesh::top_base)
-    const uint2* node_tight;    // [node][8] children's subtree triangle bounds (kTightTop above)
-    const uint2* top_tight;     // the same for the top levels, indexed like top_kids
+    const KidSlot* node_slot;   // [node][8] child entry + subtree triangle bounds (KidSlot above)
     int32_t top_mesh;          // the mesh whose top levels the walk-pool kernel stages in LDS, -1 none
     int32_t top_pad;
     float off32;                // f32 mode: hit points are offset by off32 * n (scene-scaled epsilon)

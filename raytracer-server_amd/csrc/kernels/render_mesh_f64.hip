@@ -474,9 +474,14 @@ RT_DEV bool pool2_round(const DevScene& sc, const WalkPool2& wp, LdsDouble* park
                 if (r.w.cur < 0) {
                     const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
                     fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, top);
-                } else if (walk_node(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, r.mi == sc.top_mesh ? top : nullptr,
-                                     (LdsInt*)park_i + kPark2I * kParkThreads + q) ==
-                           WALK_MISS) {
+                } else if (
+#if RT_WALK_TIGHT
+                    walk_node_slots(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, (LdsInt*)park_i + kPark2I * kParkThreads + q)
+#else
+                    walk_node(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, r.mi == sc.top_mesh ? top : nullptr,
+                              (LdsInt*)park_i + kPark2I * kParkThreads + q)
+#endif
+                    == WALK_MISS) {
                     r.w.cur = -1;  // this mesh is exhausted: the next one, if any
                 }
                 flip = !fin && r.w.cur >= 0 && r.w.lpos < r.w.lend;  // a leaf is open: triangle work next
@@ -532,7 +537,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     }
 #endif
     __shared__ double s_park_d[(P ? kPark2D : kParkD) * kParkThreads];
-    __shared__ int32_t s_park_i[(P ? kPark2I + kAncLevels : kParkI) * kParkThreads];  // pool: + ancestor ids (walk_node)
+    // pool: + ancestor ids (walk_node / walk_node_slots)
+    __shared__ int32_t s_park_i[(P ? kPark2I + (RT_WALK_TIGHT ? kSlotAncLevels : kAncLevels) : kParkI) * kParkThreads];
     const Park park{(LdsDouble*)s_park_d + threadIdx.x, (LdsInt*)s_park_i + threadIdx.x};
     // P = 1: one walk queue (s_ring[0]); P = 2: the triangle (s_ring[1]) and node (s_ring[0]) queues
     __shared__ int32_t s_ring[P == 2 ? 2 : 1][P ? 256 : 1];
@@ -547,12 +553,13 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     wp2.status = s_status;
     // pool: the top kTopDepth + 1 levels of the deepest mesh's octree in LDS (18.3 KB; the walks of
     // every query of the block start there), scene_layout.h: top_slot
-    __shared__ int4 s_top[P ? kTopNodes * 2 : 1];
+    // (the slot walk, RT_WALK_TIGHT, reads every level through the node slots: no LDS copy)
+    __shared__ int4 s_top[P && !RT_WALK_TIGHT ? kTopNodes * 2 : 1];
     const LdsTopI32* top = nullptr;
     if constexpr (P) {
         for (int j = 0; j < (P == 2 ? 2 : 1); ++j) s_ring[j][threadIdx.x] = -1;
         if (threadIdx.x < 2) { s_qhead[threadIdx.x] = 0; s_qtail[threadIdx.x] = 0; }
-        if (sc.top_mesh >= 0) {
+        if (!RT_WALK_TIGHT && sc.top_mesh >= 0) {
             const int4* src = reinterpret_cast<const int4*>(sc.top_kids + sc.meshes[sc.top_mesh].top_base);
             for (int i = threadIdx.x; i < kTopNodes * 2; i += blockDim.x) s_top[i] = src[i];
             top = (const LdsTopI32*)(LdsInt*)s_top;

@@ -190,7 +190,7 @@ RT_DEV void persistent_walks(const DevScene& sc, uint32_t n, uint32_t* head, int
         if (busy) {
             double t;
             int prim;
-            const int st = walk_step(sc, sc.meshes[q.mesh()], q.ray, q.inv, q.w, &t, &prim);
+            const int st = walk_step<false>(sc, sc.meshes[q.mesh()], q.ray, q.inv, q.w, &t, &prim);
             if (st != WALK_RUN) {
                 bool done = st == WALK_HIT && q.hit(t, prim);
                 if (!done) done = !q.next_mesh();

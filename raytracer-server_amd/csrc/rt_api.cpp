@@ -58,29 +58,25 @@ struct Packed {
     std::vector<rt::DevTri> btris;
     std::vector<int32_t> btri_id;
     std::vector<int32_t> top_kids;  // [mesh tables][kTopNodes][8]: octree top levels by position (top_slot)
-    std::vector<uint2> tight;       // [node][8] children's subtree triangle bounds (scene_layout.h kTightTop)
-    std::vector<uint2> top_tight;   // the same, indexed like top_kids
+    std::vector<rt::KidSlot> slots;      // [node][8] child entry + subtree triangle bounds (scene_layout.h KidSlot)
 };
 
-// Quantized subtree bounds of a node's children (scene_layout.h, kTightTop): per child octant, the
-// vertex bounds of every triangle in its subtree padded by `pad`, rounded OUTWARD to 8-bit codes over
-// the parent box's [mn - e, mx + e] (one extra step each way, so device-side rounding of the
-// dequantised bounds cannot move them inward). bounds: [node] lo xyz, hi xyz of the subtree.
-uint2 quantize_tight(const rt::host::Box& parent, const double* b) {
-    const double pmn[3] = {parent.min.x, parent.min.y, parent.min.z}, pmx[3] = {parent.max.x, parent.max.y, parent.max.z};
-    uint32_t lo[3], hi[3];
+// A child slot (scene_layout.h KidSlot): the child entry and its subtree's triangle bounds b (lo xyz,
+// hi xyz, already padded), rounded OUTWARD to 16-bit codes over the mesh's range (base + q * step), one
+// extra step each way so that device-side rounding of the dequantised bounds cannot move them inward.
+rt::KidSlot make_slot(int32_t kid, const rt::DevMesh& dm, const double* b) {
+    rt::KidSlot s{};
+    s.kid = kid;
     for (int k = 0; k < 3; ++k) {
-        const double e = pmx[k] - pmn[k], base = pmn[k] - e, step = rt::tight_step(e);
-        if (!(step > 0.0) || !std::isfinite(step)) {  // degenerate axis: no bound along it
-            lo[k] = 0;
-            hi[k] = rt::kTightTop;
-            continue;
-        }
-        const double ql = std::floor((b[k] - base) / step) - 1.0, qh = std::ceil((b[3 + k] - base) / step) + 1.0;
-        lo[k] = ql >= 1.0 ? (uint32_t)std::min(ql, (double)(rt::kTightTop - 1)) : 0u;
-        hi[k] = qh <= (double)(rt::kTightTop - 1) ? (uint32_t)std::max(qh, 1.0) : (uint32_t)rt::kTightTop;
+        s.lo[k] = 0;
+        s.hi[k] = (uint16_t)rt::kTightTop;
+        if (kid == rt::kKidEmpty || !(dm.tight_step > 0.0) || !std::isfinite(dm.tight_step)) continue;
+        const double ql = std::floor((b[k] - dm.tight_base[k]) / dm.tight_step) - 1.0;
+        const double qh = std::ceil((b[3 + k] - dm.tight_base[k]) / dm.tight_step) + 1.0;
+        s.lo[k] = ql >= 1.0 ? (uint16_t)std::min(ql, (double)(rt::kTightTop - 1)) : (uint16_t)0;
+        s.hi[k] = qh <= (double)(rt::kTightTop - 1) ? (uint16_t)std::max(qh, 1.0) : (uint16_t)rt::kTightTop;
     }
-    return uint2{lo[0] | lo[1] << 8 | lo[2] << 16 | hi[0] << 24, hi[1] | hi[2] << 8};
+    return s;
 }
 
 struct DeviceCopy {
@@ -408,19 +404,32 @@ int pack_scene(rt_scene* s) {
                     }
                 }
             }
+            // the 16-bit code range: the cull box's min - E .. min + 2E per axis (E its largest extent)
+            double E = 0.0;
+            for (int k = 0; k < 3; ++k) E = std::fmax(E, dm.cull_box[3 + k] - dm.cull_box[k]);
+            for (int k = 0; k < 3; ++k) dm.tight_base[k] = dm.cull_box[k] - E;
+            dm.tight_step = 3.0 * E / (double)rt::kTightTop;
+            dm.root_exist = 0;
+            if (oc.size() > 0 && !oc.kind[0])
+                for (int q = 0; q < 8; ++q) dm.root_exist |= (oc.child[q] >= 0 ? 1 : 0) << q;
             for (size_t j = 0; j < oc.size(); ++j) {
                 for (int k = 0; k < 8; ++k) {
                     const int32_t c8 = oc.child[8 * j + k];
-                    if (c8 < 0) {
-                        p.tight.push_back(uint2{0u, 0u});
-                        continue;
+                    double b[6] = {0, 0, 0, 0, 0, 0};
+                    if (c8 >= 0)
+                        for (int q = 0; q < 3; ++q) {
+                            b[q] = sb[6 * (size_t)c8 + q] - dm.cull_pad;
+                            b[3 + q] = sb[6 * (size_t)c8 + 3 + q] + dm.cull_pad;
+                        }
+                    int32_t e = p.kids[8 * (j + (size_t)dm.node_base) + k];
+                    if (e >= 0) {  // a parent: its node id and its own existence mask (KidSlot)
+                        if (e >= rt::kSlotMaxNode)
+                            return fail(RT_E_INVAL, "mesh octree too large: node ids must stay below 2^23 (scene_layout.h KidSlot)");
+                        uint32_t ex = 0;
+                        for (int q = 0; q < 8; ++q) ex |= (oc.child[8 * (size_t)c8 + q] >= 0 ? 1u : 0u) << q;
+                        e = rt::slot_parent(e, ex);
                     }
-                    double b[6];
-                    for (int q = 0; q < 3; ++q) {
-                        b[q] = sb[6 * (size_t)c8 + q] - dm.cull_pad;
-                        b[3 + q] = sb[6 * (size_t)c8 + 3 + q] + dm.cull_pad;
-                    }
-                    p.tight.push_back(quantize_tight(oc.box[j], b));
+                    p.slots.push_back(make_slot(e, dm, b));
                 }
             }
         }
@@ -429,15 +438,12 @@ int pack_scene(rt_scene* s) {
         if (oc.size() > 0 && !oc.kind[0]) {
             dm.top_base = (int32_t)p.top_kids.size();
             p.top_kids.resize(p.top_kids.size() + (size_t)rt::kTopNodes * 8, rt::kKidEmpty);
-            p.top_tight.resize(p.top_kids.size(), uint2{0u, 0u});
             int32_t* top = p.top_kids.data() + dm.top_base;
-            uint2* top_t = p.top_tight.data() + dm.top_base;
             std::function<void(int32_t, int, uint32_t)> fill = [&](int32_t node, int depth, uint32_t path) {
                 const int slot = rt::top_slot(depth, path);
                 for (int k = 0; k < 8; ++k) {
                     const int32_t e = p.kids[8 * (size_t)node + k];
                     top[8 * slot + k] = e;
-                    top_t[8 * slot + k] = p.tight[8 * (size_t)node + k];
                     if (e >= 0 && depth < rt::kTopDepth) fill(e, depth + 1, path | (uint32_t)k << (3 * depth));
                 }
             };
@@ -648,10 +654,9 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         put(blob, &o_obj32, obj32);
         put(blob, &o_bvh32, bvh32);
         put(blob, &o_tri32, tri32);
-        size_t o_top, o_tight, o_ttop;
+        size_t o_top, o_slot;
         put(blob, &o_top, p.top_kids);
-        put(blob, &o_tight, p.tight);
-        put(blob, &o_ttop, p.top_tight);
+        put(blob, &o_slot, p.slots);
         void* d = nullptr;
         HIP_TRY(hipMalloc(&d, blob.size()));
         hipError_t e = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice);
@@ -683,8 +688,7 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.compact = compact;
         // the walk-pool kernel stages the top levels of the largest octree in LDS (RT_MK_TOP=0: off, A/B)
         ds.top_kids = (const int32_t*)(b + o_top);
-        ds.node_tight = (const uint2*)(b + o_tight);
-        ds.top_tight = (const uint2*)(b + o_ttop);
+        ds.node_slot = (const rt::KidSlot*)(b + o_slot);
         ds.top_mesh = -1;
         const char* top_env = std::getenv("RT_MK_TOP");
         if (!(top_env && std::atoi(top_env) == 0)) {

@@ -28,6 +28,7 @@ struct Tight {
     std::vector<BBox> box;  // per node: union of its subtree's triangle bounds, padded
     bool after = false;     // test only children whose octant box the ray hits
     int qbits = 0;          // > 0: boxes quantized to qbits per coordinate over the parent box +- its extent
+    const BBox* qref = nullptr;  // quantise against this box (the mesh's) instead of the parent's
 };
 // conservative quantization of child box c inside parent box b's range [b.min - e, b.max + e]
 BBox quant(const BBox& c, const BBox& b, int bits) {
@@ -128,7 +129,7 @@ bool walk(const Mesh& m, int ni, BBox box, const Ray& ray, Hit* h, int* tri, Cou
             BBox oc = octant(box, i);
             auto tcull = [&]() {
                 if (!T) return false;
-                const BBox tb = T->qbits ? quant(T->box[node.children[i]], box, T->qbits) : T->box[node.children[i]];
+                const BBox tb = T->qbits ? quant(T->box[node.children[i]], T->qref ? *T->qref : box, T->qbits) : T->box[node.children[i]];
                 return !near(tb, ray, pad);
             };
             if (T && !T->after && tcull()) {
@@ -230,7 +231,7 @@ int main(int argc, char** argv) {
     Tight T2 = T, T3 = T, T4 = T;
     T2.after = true;
     T3.after = true; T3.qbits = 8;
-    T4.after = true; T4.qbits = 16;
+    T4.after = true; T4.qbits = 16; T4.qref = &M.bbox;
     Counts base, tight, after, q8, q16;
     long past = 0;
     for (const Ray& r : Q) {
@@ -261,7 +262,7 @@ int main(int argc, char** argv) {
     pr("tight", tight);
     pr("after", after);
     pr("q8", q8);
-    pr("q16", q16);
+    pr("q16 mesh", q16);
     std::printf("f32 octant classification (margin 1e-5 of the box extent): %ld tests, %.4f ambiguous\n", base.f32_tests,
                 (double)base.f32_amb / std::max(1L, base.f32_tests));
     return 0;
