@@ -829,6 +829,9 @@ RT_DEV int4 kid_slot(const DevScene& sc, int32_t cur, uint32_t oi) {
 // ancestor node ids at depths 0 .. kSlotAncLevels - 1 (stride 256 threads), written at each descent,
 // so a pop reads the node it resumes at from LDS.
 constexpr int kSlotAncLevels = 9;
+#ifndef RT_POP_BOXLOAD
+#define RT_POP_BOXLOAD 1  // A/B: a pop reloads the ancestor's box (1) or rebuilds it from the root (0)
+#endif
 #ifndef RT_SLOT_CULL
 #define RT_SLOT_CULL 1  // A/B: 0 = the slot walk without the subtree-bounds test
 #endif  // the deepest parents sit at depth 8 (MAX_DEPTH 10, root depth 1)
@@ -856,6 +859,14 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
         w.depth = lv;
         w.pm = pm;
         w.path &= (1u << (3 * lv)) - 1u;
+#if RT_POP_BOXLOAD
+        // the ancestor's box (DevScene::node_box: the same arithmetic as the descents); only a descent
+        // from it reads the box, so the load overlaps the pick's slot load
+        const double2* nb = reinterpret_cast<const double2*>(sc.node_box + 6 * (size_t)w.cur);
+        const double2 b0 = nb[0], b1 = nb[1], b2 = nb[2];
+        w.mn[0] = b0.x; w.mn[1] = b0.y; w.mn[2] = b1.x;
+        w.mx[0] = b1.y; w.mx[1] = b2.x; w.mx[2] = b2.y;
+#else
         // the ancestor's box, rebuilt from the root along the path (the build's own arithmetic)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -870,6 +881,7 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
                 if ((oi >> (2 - k)) & 1u) w.mn[k] = c; else w.mx[k] = c;
             }
         }
+#endif
     }
     RT_DBG_TEND(13, t_pop);
     RT_DBG_TSTART(t_pick);

@@ -201,6 +201,8 @@ struct DevScene {
     const Compact32* ctab32;    // f32 compact tables (ok == 0: the generic object loop)
     const int32_t* top_kids;    // top-levels child tables of the meshes (DevMesh::top_base)
     const KidSlot* node_slot;   // [node][8] child entry + subtree triangle bounds (KidSlot above)
+    const double* node_box;     // [node][6] the node's octant box (min xyz, max xyz) with the walk's own
+                                // arithmetic: a pop of the slot walk reloads the ancestor's box from here
     int32_t top_mesh;          // the mesh whose top levels the walk-pool kernel stages in LDS, -1 none
     int32_t top_pad;
     float off32;                // f32 mode: hit points are offset by off32 * n (scene-scaled epsilon)

@@ -59,6 +59,7 @@ struct Packed {
     std::vector<int32_t> btri_id;
     std::vector<int32_t> top_kids;  // [mesh tables][kTopNodes][8]: octree top levels by position (top_slot)
     std::vector<rt::KidSlot> slots;      // [node][8] child entry + subtree triangle bounds (scene_layout.h KidSlot)
+    std::vector<double> node_box;        // [node][6] octant boxes, the walk's arithmetic (DevScene::node_box)
 };
 
 // A child slot (scene_layout.h KidSlot): the child entry and its subtree's triangle bounds b (lo xyz,
@@ -404,6 +405,25 @@ int pack_scene(rt_scene* s) {
                     }
                 }
             }
+            // every node's box as the walk computes it: the root box, then per level the octant of the
+            // parent's box with c = (mn + mx) / 2 (path_f64.h walk_node_slots; DFS pre-order: parents first)
+            const size_t nb0 = p.node_box.size();
+            p.node_box.resize(nb0 + 6 * oc.size());
+            double* nb = p.node_box.data() + nb0;
+            for (size_t j = 0; j < oc.size(); ++j) {
+                if (oc.parent[j] < 0) {
+                    std::memcpy(nb + 6 * j, rbox, sizeof rbox);
+                    continue;
+                }
+                const double* pb = nb + 6 * (size_t)oc.parent[j];
+                const uint32_t oi = (uint32_t)oc.slot[j];
+                for (int k = 0; k < 3; ++k) {
+                    const double c = (pb[k] + pb[3 + k]) / 2.0;
+                    const bool hi = ((oi >> (2 - k)) & 1u) != 0;
+                    nb[6 * j + k] = hi ? c : pb[k];
+                    nb[6 * j + 3 + k] = hi ? pb[3 + k] : c;
+                }
+            }
             // the 16-bit code range: the cull box's min - E .. min + 2E per axis (E its largest extent)
             double E = 0.0;
             for (int k = 0; k < 3; ++k) E = std::fmax(E, dm.cull_box[3 + k] - dm.cull_box[k]);
@@ -657,6 +677,8 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         size_t o_top, o_slot;
         put(blob, &o_top, p.top_kids);
         put(blob, &o_slot, p.slots);
+        size_t o_nbox;
+        put(blob, &o_nbox, p.node_box);
         void* d = nullptr;
         HIP_TRY(hipMalloc(&d, blob.size()));
         hipError_t e = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice);
@@ -689,6 +711,7 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         // the walk-pool kernel stages the top levels of the largest octree in LDS (RT_MK_TOP=0: off, A/B)
         ds.top_kids = (const int32_t*)(b + o_top);
         ds.node_slot = (const rt::KidSlot*)(b + o_slot);
+        ds.node_box = (const double*)(b + o_nbox);
         ds.top_mesh = -1;
         const char* top_env = std::getenv("RT_MK_TOP");
         if (!(top_env && std::atoi(top_env) == 0)) {
