@@ -573,6 +573,10 @@ struct OctWalk {
     int32_t lpos, lend;   // leaf triangle cursor
     int32_t best;         // nearest triangle so far in the current leaf (ltri index), -1 none
     double bt;
+    // The slot walk's one-leaf buffer (walk_step<true>): the next leaf in visiting order the node walk
+    // found while the cursor was still busy (nlf < nle), and whether the node walk is exhausted.
+    int32_t nlf, nle;
+    uint32_t ndone;
     // Read-ahead of the next descent (the walk's dependent load chain: pick a child entry -> load that
     // node's 8 child entries -> octant_mask -> pick ...): walk_enter takes the entry of the first child
     // in visiting order from the node's child table it has in registers (nc), and when that child is
@@ -674,6 +678,8 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
     RT_DBG(1);
     w.best = -1;
     w.bt = 0.0;
+    w.nlf = w.nle = 0;
+    w.ndone = 0;
     w.cur = m.node_base;
     w.depth = 0;
     w.path = 0;
@@ -913,9 +919,14 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
             first = ls.x;
             cnt = ls.y;
         }
-        w.lpos = first;
-        w.lend = first + cnt;
-        w.best = -1;
+        if (w.lpos >= w.lend) {  // the triangle cursor is free: test this leaf next
+            w.lpos = first;
+            w.lend = first + cnt;
+            w.best = -1;
+        } else {  // the cursor is still on an earlier leaf: buffer this one (walk_step<true>)
+            w.nlf = first;
+            w.nle = first + cnt;
+        }
         RT_DBG_TEND(14, t_pick);
         return WALK_RUN;
     }
@@ -1030,13 +1041,37 @@ template <bool Slots = (RT_WALK_TIGHT != 0)>
 RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w, double* t,
                      int* prim, const LdsTopI32* top = nullptr, LdsTopI32* anc = nullptr) {
     RT_DBG(5);
+    if constexpr (Slots) {
+        // The node walk and the triangle tests run in the same step, one leaf apart: the node walk
+        // advances (pop / pick / descend) while no found leaf waits in the buffer, and the open leaf's
+        // next triangles are tested. Leaves are still tested in visiting order and the first leaf with
+        // a hit ends the walk (a leaf the node walk found beyond it is dropped): the same result, in
+        // fewer steps, with both parts of a step busy in most lanes.
+        (void)top;
+        if (!w.ndone && w.nlf >= w.nle && walk_node_slots(sc, m, ray, inv, w, anc) == WALK_MISS) w.ndone = 1;
+        RT_DBG_TSTART(t_lt);
+        if (w.lpos < w.lend) {
+            const int st = leaf_tris(sc, ray, w, t, prim);
+            if (st == WALK_HIT) {
+                RT_DBG_TEND(12, t_lt);
+                return WALK_HIT;
+            }
+            if (st < 0 && w.nlf < w.nle) {  // leaf done without a hit: the buffered one is next
+                w.lpos = w.nlf;
+                w.lend = w.nle;
+                w.best = -1;
+                w.nle = w.nlf;
+            }
+        }
+        RT_DBG_TEND(12, t_lt);
+        return w.ndone && w.lpos >= w.lend && w.nlf >= w.nle ? WALK_MISS : WALK_RUN;
+    }
     int st = -1;
     RT_DBG_TSTART(t_lt);
     if (w.lpos < w.lend) st = leaf_tris(sc, ray, w, t, prim);  // triangles of the open leaf
     RT_DBG_TEND(12, t_lt);
     if (st >= 0) return st;
-    if constexpr (Slots) st = walk_node_slots(sc, m, ray, inv, w, anc);
-    else st = walk_node(sc, m, ray, inv, w, top, anc);
+    st = walk_node(sc, m, ray, inv, w, top, anc);
 #if RT_WALK_OPEN_TEST
     if (st == WALK_RUN && w.lpos < w.lend) {  // a leaf was just opened: its first triangles in this step
         const int s2 = leaf_tris(sc, ray, w, t, prim);

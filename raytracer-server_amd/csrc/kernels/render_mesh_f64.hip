@@ -54,7 +54,7 @@ enum : int { PH_TRACE = 0, PH_WALK_CLOSEST = 1, PH_WALK_SHADOW = 2 };
 // the walk phase holds only the path state plus the walk (no scratch spills at 2 waves/SIMD).
 // Doubles: ray o, d; 1/d; box mn, mx; walk best t; query t (closest hit so far / shadow distance);
 // pending NEE term. Ints: walk cursor fields, closest hit object/prim, gen slot, mesh, occluded.
-constexpr int kParkD = 21, kParkI = 16, kParkThreads = 256;
+constexpr int kParkD = 21, kParkI = 18, kParkThreads = 256;
 struct Park {  // typed in the LDS address space: ds_read/ds_write with one 32-bit base + immediate offsets
     LdsDouble* d;  // this thread's column of [kParkD][kParkThreads]
     LdsInt* i;     // [kParkI][kParkThreads]
@@ -75,10 +75,11 @@ RT_DEV void park_store(const Park& p, const WalkRegs& r) {
     for (int k = 0; k < 3; ++k) { p.D(9 + k) = r.w.mn[k]; p.D(12 + k) = r.w.mx[k]; }
     p.D(15) = r.w.bt;
     p.D(16) = r.wt;
-    p.I(0) = r.w.cur; p.I(1) = r.w.depth; p.I(2) = (int32_t)r.w.path; p.I(3) = (int32_t)r.w.pm;
+    p.I(0) = r.w.cur; p.I(1) = r.w.depth | (int32_t)(r.w.ndone << 24); p.I(2) = (int32_t)r.w.path; p.I(3) = (int32_t)r.w.pm;
     p.I(4) = (int32_t)(uint32_t)r.w.stk; p.I(5) = (int32_t)(uint32_t)(r.w.stk >> 32); p.I(6) = (int32_t)r.w.stk8;
     p.I(7) = (int32_t)r.w.order; p.I(8) = r.w.lpos; p.I(9) = r.w.lend; p.I(10) = r.w.best;
     p.I(11) = r.hobj; p.I(12) = r.hprim; p.I(13) = r.g; p.I(14) = r.mi; p.I(15) = r.occluded;
+    p.I(16) = r.w.nlf; p.I(17) = r.w.nle;
 }
 RT_DEV void park_load(const Park& p, WalkRegs& r) {
     r.wr.o = v3(p.D(0), p.D(1), p.D(2));
@@ -87,10 +88,12 @@ RT_DEV void park_load(const Park& p, WalkRegs& r) {
     for (int k = 0; k < 3; ++k) { r.w.mn[k] = p.D(9 + k); r.w.mx[k] = p.D(12 + k); }
     r.w.bt = p.D(15);
     r.wt = p.D(16);
-    r.w.cur = p.I(0); r.w.depth = p.I(1); r.w.path = (uint32_t)p.I(2); r.w.pm = (uint32_t)p.I(3);
+    r.w.cur = p.I(0); r.w.depth = p.I(1) & 0xFF; r.w.ndone = (uint32_t)p.I(1) >> 24; r.w.path = (uint32_t)p.I(2);
+    r.w.pm = (uint32_t)p.I(3);
     r.w.stk = (uint64_t)(uint32_t)p.I(4) | ((uint64_t)(uint32_t)p.I(5) << 32); r.w.stk8 = (uint32_t)p.I(6);
     r.w.order = (uint32_t)p.I(7); r.w.lpos = p.I(8); r.w.lend = p.I(9); r.w.best = p.I(10);
     r.hobj = p.I(11); r.hprim = p.I(12); r.g = p.I(13); r.mi = p.I(14); r.occluded = p.I(15);
+    r.w.nlf = p.I(16); r.w.nle = p.I(17);
     r.w.nc = kNcNone;  // the read-ahead is not parked here: the next pick reads its entry
 }
 
@@ -276,7 +279,7 @@ constexpr int kPoolRefill = 8;  // refill only when at least this many lanes of 
 // registers), depth / pm / stk8 packed in one word. Doubles: ray o, d; box mn, mx; walk best t;
 // query t (closest hit so far / shadow distance). Ints: cur, depth | pm << 8 | stk8 << 16, path,
 // stk (2 words), order, lpos, lend, best, hit object, hit prim, gen slot, mesh, occluded.
-constexpr int kPark2D = 14, kPark2I = RT_WALK_READAHEAD ? 15 : 14;
+constexpr int kPark2D = 14, kPark2I = RT_WALK_READAHEAD ? 17 : 16;
 enum : int { P2_T = 13, P2_HOBJ = 9, P2_HPRIM = 10, P2_OCC = 13 };
 RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
     p.D(0) = r.wr.o.x; p.D(1) = r.wr.o.y; p.D(2) = r.wr.o.z;
@@ -285,13 +288,14 @@ RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
     p.D(12) = r.w.bt;
     p.D(13) = r.wt;
     p.I(0) = r.w.cur;
-    p.I(1) = (int32_t)((uint32_t)r.w.depth | (r.w.pm << 8) | (r.w.stk8 << 16));
+    p.I(1) = (int32_t)((uint32_t)r.w.depth | (r.w.pm << 8) | (r.w.stk8 << 16) | (r.w.ndone << 24));
     p.I(2) = (int32_t)r.w.path;
     p.I(3) = (int32_t)(uint32_t)r.w.stk; p.I(4) = (int32_t)(uint32_t)(r.w.stk >> 32);
     p.I(5) = (int32_t)r.w.order; p.I(6) = r.w.lpos; p.I(7) = r.w.lend; p.I(8) = r.w.best;
     p.I(9) = r.hobj; p.I(10) = r.hprim; p.I(11) = r.g; p.I(12) = r.mi; p.I(13) = r.occluded;
+    p.I(14) = r.w.nlf; p.I(15) = r.w.nle;
 #if RT_WALK_READAHEAD
-    p.I(14) = r.w.nc;
+    p.I(16) = r.w.nc;
 #endif
 }
 RT_DEV void park2_load(const Park& p, WalkRegs& r) {
@@ -303,13 +307,14 @@ RT_DEV void park2_load(const Park& p, WalkRegs& r) {
     r.wt = p.D(13);
     r.w.cur = p.I(0);
     const uint32_t dps = (uint32_t)p.I(1);
-    r.w.depth = (int32_t)(dps & 0xFFu); r.w.pm = (dps >> 8) & 0xFFu; r.w.stk8 = dps >> 16;
+    r.w.depth = (int32_t)(dps & 0xFFu); r.w.pm = (dps >> 8) & 0xFFu; r.w.stk8 = (dps >> 16) & 0xFFu; r.w.ndone = dps >> 24;
     r.w.path = (uint32_t)p.I(2);
     r.w.stk = (uint64_t)(uint32_t)p.I(3) | ((uint64_t)(uint32_t)p.I(4) << 32);
     r.w.order = (uint32_t)p.I(5); r.w.lpos = p.I(6); r.w.lend = p.I(7); r.w.best = p.I(8);
     r.hobj = p.I(9); r.hprim = p.I(10); r.g = p.I(11); r.mi = p.I(12); r.occluded = p.I(13);
+    r.w.nlf = p.I(14); r.w.nle = p.I(15);
 #if RT_WALK_READAHEAD
-    r.w.nc = p.I(14);  // its child entries are loaded again by walk_reload_ahead
+    r.w.nc = p.I(16);  // its child entries are loaded again by walk_reload_ahead
 #else
     r.w.nc = kNcNone;
 #endif
@@ -322,7 +327,7 @@ RT_DEV void park2_query(const Park& p, const Ray& r, double wt, int32_t hobj, in
     p.I(0) = -1;
     p.I(9) = hobj; p.I(10) = hprim; p.I(11) = -1; p.I(13) = 0;
 #if RT_WALK_READAHEAD
-    p.I(14) = kNcNone;
+    p.I(16) = kNcNone;
 #endif
 }
 
