@@ -414,114 +414,6 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
     return true;
 }
 
-// Two-queue walk pool (P = 2): a walk alternates between triangle work (its open leaf's triangles,
-// leaf_tris) and node work (pop exhausted levels, pick the next child, open it or descend and mask its
-// children: walk_node; also a walk's start), and the two cost differently (a leaf step tests 2
-// triangles, a descent evaluates the 9 planes of octant_mask). With one queue a wave's 64 walks need
-// both kinds in every step and the wave pays for both with part of its lanes idle. Here each query
-// sits in the queue of the work it needs next (qt: triangles, qn: nodes); a wave takes a batch from
-// one queue and runs only that kind of step, so its lanes run the same code. A walk whose next work
-// changes kind is parked and moved to the other queue, its lane refilled from the round's queue.
-// Same steps, same order within each walk: same results as the one-queue pool (tested).
-struct WalkPool2 {
-    LdsQueue qt, qn;    // 256-entry rings: each query is in at most one of them
-    uint8_t* status;    // as WalkPool
-};
-template <class C>
-RT_DEV bool pool2_round(const DevScene& sc, const WalkPool2& wp, LdsDouble* park_d, LdsInt* park_i, int need,
-                        int ksteps, const LdsTopI32* top) {
-    // serve the longer queue that has `need` entries (wave-uniform lengths)
-    const uint32_t lt = __builtin_amdgcn_readfirstlane(queue_len(wp.qt));
-    const uint32_t ln = __builtin_amdgcn_readfirstlane(queue_len(wp.qn));
-    bool tq = lt > ln;
-    int32_t q = queue_take(tq ? wp.qt : wp.qn, need);
-    if (!__any(q >= 0)) {
-        tq = !tq;
-        q = queue_take(tq ? wp.qt : wp.qn, need);
-        if (!__any(q >= 0)) return false;
-    }
-    const LdsQueue& Q = tq ? wp.qt : wp.qn;
-    const LdsQueue& O = tq ? wp.qn : wp.qt;
-    WalkRegs r;
-    bool closest = false;
-    auto col = [&](int32_t c) { return Park{park_d + c, park_i + c}; };
-    if (q >= 0) {
-        park2_load(col(q), r);
-        if (r.w.cur >= 0) walk_reload_ahead(sc, r.w, r.mi == sc.top_mesh ? top : nullptr);
-        const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        closest = stq == POOL_CLOSEST;
-        if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
-    }
-    for (int k = 0; k < ksteps; ++k) {
-        RT_DBG_WAVE(10, lane_id_is0());
-        RT_DBG_WAVE(11, q >= 0);
-        bool fin = false, flip = false;
-        if (q >= 0) {
-            if (tq) {  // triangle work: up to kTrisPerStep triangles of the open leaf
-                double t;
-                int prim;
-                const int st = leaf_tris(sc, r.wr, r.w, &t, &prim);
-                if (st == WALK_HIT) {  // the first subtree with a hit: this mesh's result
-                    if (closest) {
-                        HitRec h{r.wt, r.hobj, r.hprim};
-                        consider(h, t, tables(sc)->gen_idx[r.g], prim);
-                        r.wt = h.t;
-                        r.hobj = h.obj;
-                        r.hprim = h.prim;
-                    } else {
-                        r.occluded = !(t + 0.001 >= r.wt);  // mutually_visible's ERR_MARGIN
-                        fin = r.occluded;
-                    }
-                    r.w.cur = -1;  // next: the next mesh, if any (node work)
-                }
-                flip = !fin && st != WALK_RUN;  // leaf done: node work next
-            } else {  // node work: a walk's start, or pop + pick (+ descend)
-                if (r.w.cur < 0) {
-                    const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
-                    fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, top);
-                } else if (
-#if RT_WALK_TIGHT
-                    walk_node_slots(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, (LdsInt*)park_i + kPark2I * kParkThreads + q)
-#else
-                    walk_node(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, r.mi == sc.top_mesh ? top : nullptr,
-                              (LdsInt*)park_i + kPark2I * kParkThreads + q)
-#endif
-                    == WALK_MISS) {
-                    r.w.cur = -1;  // this mesh is exhausted: the next one, if any
-                }
-                flip = !fin && r.w.cur >= 0 && r.w.lpos < r.w.lend;  // a leaf is open: triangle work next
-            }
-            if (fin) {  // results for the owner's vertex phase, then the status word
-                const Park pq = col(q);
-                pq.D(P2_T) = r.wt;
-                pq.I(P2_HOBJ) = r.hobj;
-                pq.I(P2_HPRIM) = r.hprim;
-                pq.I(P2_OCC) = r.occluded;
-                __hip_atomic_store(&wp.status[q], (uint8_t)POOL_DONE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                q = -1;
-            } else if (flip) {
-                park2_store(col(q), r);
-            }
-        }
-        queue_put(O, flip, q);  // the walks whose next work is the other kind
-        if (flip) q = -1;
-        if (k + 1 < ksteps && __popcll(__ballot(q < 0)) >= kPoolRefill) {
-            const int32_t q2 = queue_take_each(Q, q < 0);
-            if (q2 >= 0) {
-                q = q2;
-                park2_load(col(q), r);
-        if (r.w.cur >= 0) walk_reload_ahead(sc, r.w, r.mi == sc.top_mesh ? top : nullptr);
-                const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                closest = stq == POOL_CLOSEST;
-                if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
-            }
-        }
-    }
-    if (q >= 0) park2_store(col(q), r);
-    queue_put(Q, q >= 0, q);
-    return true;
-}
-
 template <int F, int W, int P>
 __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
                                                                uint32_t* next_sub, long nsub, int ksteps, int wmin,
@@ -545,24 +437,20 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     // pool: + ancestor ids (walk_node / walk_node_slots)
     __shared__ int32_t s_park_i[(P ? kPark2I + (RT_WALK_TIGHT ? kSlotAncLevels : kAncLevels) : kParkI) * kParkThreads];
     const Park park{(LdsDouble*)s_park_d + threadIdx.x, (LdsInt*)s_park_i + threadIdx.x};
-    // P = 1: one walk queue (s_ring[0]); P = 2: the triangle (s_ring[1]) and node (s_ring[0]) queues
-    __shared__ int32_t s_ring[P == 2 ? 2 : 1][P ? 256 : 1];
+    // P = 1: one walk queue
+    __shared__ int32_t s_ring[1][P ? 256 : 1];
     __shared__ uint8_t s_status[P ? 256 : 1];
     __shared__ uint32_t s_qhead[2], s_qtail[2];
     WalkPool wp;
     wp.q = LdsQueue{s_ring[0], s_qhead, s_qtail, 255u};
     wp.status = s_status;
-    WalkPool2 wp2;
-    wp2.qt = LdsQueue{s_ring[P == 2 ? 1 : 0], s_qhead + 1, s_qtail + 1, 255u};
-    wp2.qn = wp.q;
-    wp2.status = s_status;
     // pool: the top kTopDepth + 1 levels of the deepest mesh's octree in LDS (18.3 KB; the walks of
     // every query of the block start there), scene_layout.h: top_slot
     // (the slot walk, RT_WALK_TIGHT, reads every level through the node slots: no LDS copy)
     __shared__ int4 s_top[P && !RT_WALK_TIGHT ? kTopNodes * 2 : 1];
     const LdsTopI32* top = nullptr;
     if constexpr (P) {
-        for (int j = 0; j < (P == 2 ? 2 : 1); ++j) s_ring[j][threadIdx.x] = -1;
+        s_ring[0][threadIdx.x] = -1;
         if (threadIdx.x < 2) { s_qhead[threadIdx.x] = 0; s_qtail[threadIdx.x] = 0; }
         if (!RT_WALK_TIGHT && sc.top_mesh >= 0) {
             const int4* src = reinterpret_cast<const int4*>(sc.top_kids + sc.meshes[sc.top_mesh].top_base);
@@ -603,10 +491,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
         if constexpr (P) {
             // take queued queries (at least pool_min of them while this wave has paths to shade)
             const int ready = __popcll(__ballot(active && !walking));
-            if constexpr (P == 2)
-                took = pool2_round<C>(sc, wp2, (LdsDouble*)s_park_d, (LdsInt*)s_park_i, ready ? pool_min : 1, ksteps, top);
-            else
-                took = pool_round<C>(sc, wp, (LdsDouble*)s_park_d, (LdsInt*)s_park_i, ready ? pool_min : 1, ksteps, top);
+            took = pool_round<C>(sc, wp, (LdsDouble*)s_park_d, (LdsInt*)s_park_i, ready ? pool_min : 1, ksteps, top);
             if (!took && !ready) {
                 __builtin_amdgcn_s_sleep(2);  // every path of this wave waits on walks other waves hold
             }
@@ -771,7 +656,6 @@ hipError_t launch_megakernel_mesh_f64(const DevScene& sc, const RenderArgs& a, d
 #define RT_MM_CASE(F)                                                                          \
     case F:                                                                                    \
         if (pool == 3) launch_mm<F, 3, 1>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
-        else if (pool == 2) launch_mm<F, 2, 2>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
         else if (pool) launch_mm<F, 2, 1>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
         else launch_mm<F, 2, 0>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, 0, 0, tail_buf, tail_cap, st); \
         break;
