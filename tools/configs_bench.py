@@ -1,15 +1,32 @@
 """Every BASELINE.json config on one GPU (one process): Msamples/s per config, device time.
-python tools/configs_bench.py [--quick] [--fp32]  (--fp32: the f32 perf mode; C5 is 4096x4096 at reduced spp on 1 GPU: stated in the line)"""
+
+python tools/configs_bench.py [--quick] [--fp32] [--json]
+  --fp32  the f32 perf mode
+  --json  one bench-style JSON line per config instead of the text line: value, roofline (SURVEY §8(d):
+          88 B per camera sample + 280 B per path vertex over the device time; for mesh scenes also the
+          scene bytes touched, 32 B per parent visit + 8 B per leaf + (4 + 36) B per triangle test, from
+          the walk counters of the diagnostic build lib/variants/dbg.so run in a subprocess at 16 spp;
+          and the compute block from the scene's committed PMC summary profiles/<round>_pmc_<scene>_*.json)
+          and cpu_baseline (the config's line in profiles/r03_cpu_configs.log, tools/cpu_configs.py)
+C5 is 4096x4096 at 64 of its 4096 spp on 1 GPU (stated in the line; the per-rank share at full spp is
+tools/tail_probe.py share ...)."""
+import glob
+import json
 import os
+import subprocess
 import sys
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "raytracer-server_amd"))
+sys.path.insert(0, REPO)
 import rt_amd  # noqa: E402
+
+import bench  # noqa: E402  (compute_block, constants)
 
 quick = "--quick" in sys.argv
 fp32 = "--fp32" in sys.argv
+as_json = "--json" in sys.argv
 CONFIGS = [
     # (label, scene, w, h, spp, mis)
     ("C1 cornell 600x450 1spp (reference plumbing case: black frame)", "cornell_box", 600, 450, 1, False),
@@ -21,7 +38,60 @@ CONFIGS = [
     ("C4 unicorn 1920x1080 512spp", "flying_unicorn", 1920, 1080, 512, False),
     ("C5 unicorn 4096x4096 (64 of 4096 spp, 1 GPU)", "flying_unicorn", 4096, 4096, 64, False),
 ]
+
+_WALK_SCRIPT = r"""
+import ctypes, json, os, sys
+sys.path.insert(0, os.path.join(os.environ["RT_REPO"], "raytracer-server_amd"))
+import rt_amd
+s = rt_amd.Scene.from_toml(os.path.join(os.environ["RT_REPO"], "scenes", sys.argv[1] + ".toml"))
+c = (ctypes.c_ulonglong * 16)()
+rt_amd.render(s, 64, 48, 4, megakernel=True)
+rt_amd.lib.rt_debug_counters(c)
+_, _, st = rt_amd.render(s, int(sys.argv[2]), int(sys.argv[3]), 16, megakernel=True, mis=sys.argv[4] == "1")
+rt_amd.lib.rt_debug_counters(c)
+print(json.dumps({"calls": c[0], "parent_visits": c[2], "leaves": c[3], "tri_tests": c[4], "vertices": st["vertices"],
+                  "samples": st["samples"]}))
+"""
+
+
+def walk_counters(scene, w, h, mis):
+    """Per-vertex octree walk counters of the diagnostic build (None if it is not built)."""
+    lib = os.path.join(REPO, "raytracer-server_amd", "lib", "variants", "dbg.so")
+    if not os.path.exists(lib):
+        return None
+    env = dict(os.environ, RT_AMD_LIB=lib, RT_REPO=REPO)
+    out = subprocess.run([sys.executable, "-c", _WALK_SCRIPT, scene, str(w), str(h), "1" if mis else "0"], env=env,
+                         capture_output=True, text=True, timeout=300)
+    if out.returncode != 0:
+        return None
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def pmc_mix(scene, mis):
+    """The newest committed PMC instruction mix of this scene's megakernel (tools/pmc_report.py)."""
+    pat = os.path.join(REPO, "profiles", f"r*_pmc_{scene}_*{'_mis' if mis else ''}.json")
+    files = sorted(f for f in glob.glob(pat) if mis or "_mis" not in os.path.basename(f))
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+            if d.get("valu_mix"):
+                return d["valu_mix"], os.path.relpath(f, REPO)
+        except (OSError, ValueError):
+            continue
+    return None, None
+
+
+def cpu_rates():
+    try:
+        with open(os.path.join(REPO, "profiles", "r03_cpu_configs.log")) as f:
+            return {d["config"]: d for d in (json.loads(x) for x in f if x.startswith("{"))}
+    except (OSError, ValueError):
+        return {}
+
+
 scenes = {}
+cpu = cpu_rates() if as_json else {}
 for label, name, w, h, spp, mis in CONFIGS:
     if quick:
         spp = max(1, spp // 16) if spp > 4 else spp
@@ -32,6 +102,46 @@ for label, name, w, h, spp, mis in CONFIGS:
     wall = time.perf_counter() - t
     n = st["samples"]
     rate = n / st["device_ms"] / 1e3 if st["device_ms"] > 0 and n else 0.0
-    print(f"{label}{' [f32]' if fp32 else ''}: spp {spp}, {n} samples, {st['device_ms']:.1f} ms device, {wall*1e3:.1f} ms wall, "
-          f"{rate:.1f} Msamples/s, {st['vertices'] / max(1, n):.3f} vertices/sample, mean RGB8 {rgb.mean():.2f}",
-          flush=True)
+    if not as_json:
+        print(f"{label}{' [f32]' if fp32 else ''}: spp {spp}, {n} samples, {st['device_ms']:.1f} ms device, {wall*1e3:.1f} ms wall, "
+              f"{rate:.1f} Msamples/s, {st['vertices'] / max(1, n):.3f} vertices/sample, mean RGB8 {rgb.mean():.2f}",
+              flush=True)
+        continue
+    if n == 0:
+        print(json.dumps({"config": label, "value": 0.0, "unit": "Msamples/s", "note": "spp/4 = 0: no samples"}), flush=True)
+        continue
+    sec = st["device_ms"] / 1e3
+    model = bench.BYTES_PER_SAMPLE * n + bench.BYTES_PER_VERTEX * st["vertices"]
+    line = {"metric": f"Msamples/sec {name} {w}x{h}x{spp}spp{' mis' if mis else ''}", "config_label": label,
+            "value": round(rate, 3), "unit": "Msamples/s", "n_gpus": 1, "higher_is_better": True,
+            "dtype": "f32" if fp32 else "f64", "data": "synthetic: reference scene file + counter-based RNG, seed 0x5eed",
+            "config": {"workload": f"{name} {w}x{h}x{spp}spp", "scene": f"scenes/{name}.toml", "width": w, "height": h,
+                       "spp": spp, "mis": mis, "mode": "megakernel" + ("-f32" if fp32 else ""),
+                       "vertices": st["vertices"], "vertices_per_sample": round(st["vertices"] / n, 4),
+                       "device_ms": round(st["device_ms"], 3)},
+            "roofline": {"bound": "hbm", "achieved": round(model / sec / 1e9, 2), "peak": bench.HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(model / sec / 1e9 / bench.HBM_PEAK_GBS, 4), "traffic": None,
+                         "algorithmic_bytes_per_launch": model,
+                         "algorithmic_model": "SURVEY 8(d): 88 B per camera sample + 280 B per path vertex"}}
+    if name != "cornell_box" and not fp32:
+        wc = walk_counters(name, min(w, 1920), min(h, 1080), mis)
+        if wc and wc["vertices"] and wc["calls"]:  # (flat meshes, the cubes: flat_query, no walk counters)
+            per_v = {k: wc[k] / wc["vertices"] for k in ("calls", "parent_visits", "leaves", "tri_tests")}
+            sb_v = 32 * per_v["parent_visits"] + 8 * per_v["leaves"] + 40 * per_v["tri_tests"]
+            line["roofline"]["scene_bytes"] = {
+                "model": "SURVEY 8(d): 32 B per parent visit + 8 B per leaf + (4 + 36) B per triangle test (LDS / L2 / MALL, "
+                         "not HBM)",
+                "per_vertex": round(sb_v, 2), "GBps": round(sb_v * st["vertices"] / sec / 1e9, 2),
+                "walks_per_vertex": round(per_v["calls"], 4),
+                "per_walk": {k: round(wc[k] / max(1, wc["calls"]), 3) for k in ("parent_visits", "leaves", "tri_tests")},
+                "source": "walk counters of lib/variants/dbg.so (RT_DEBUG_COUNTERS) on the same scene at 16 spp"}
+    mix, src = pmc_mix(name, mis)
+    if mix and not fp32:
+        line["roofline"]["compute"] = bench.compute_block(mix, st["vertices"], st["device_ms"])
+        line["roofline"]["compute"]["source"] = src
+    c = cpu.get(label.split(" (")[0]) or next((v for k, v in cpu.items() if k.startswith(label.split(" (")[0])), None)
+    if c:
+        line["cpu_baseline"] = {"value": c["all_cores"]["Msamples_per_s"], "unit": "Msamples/s", "cores": c["cores"],
+                                "kind": c["kind"], "sample": c["all_cores"]["sample"],
+                                "single_thread": c["one_thread"], "source": "profiles/r03_cpu_configs.log"}
+    print(json.dumps(line), flush=True)
