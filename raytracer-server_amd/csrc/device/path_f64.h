@@ -577,6 +577,8 @@ struct OctWalk {
     // found while the cursor was still busy (nlf < nle), and whether the node walk is exhausted.
     int32_t nlf, nle;
     uint32_t ndone;
+    uint32_t enter;  // slot walk: the root is still to be entered (its octant_mask runs in the first step,
+                     // in the same code as every descent's)
     // Read-ahead of the next descent (the walk's dependent load chain: pick a child entry -> load that
     // node's 8 child entries -> octant_mask -> pick ...): walk_enter takes the entry of the first child
     // in visiting order from the node's child table it has in registers (nc), and when that child is
@@ -670,6 +672,9 @@ RT_DEV void walk_reload_ahead(const DevScene& sc, OctWalk& w, const LdsTopI32* t
 
 // Starts a walk; false if the ray cannot produce a usable hit on this mesh (empty mesh, or the
 // conservative near_box cull). tmax: see near_box.
+// Slots: the walk continues with walk_step<true> (the slot walk: the root is entered in its first step),
+// or with walk_step<false> (the node_kids walk: entered here).
+template <bool Slots = (RT_WALK_TIGHT != 0)>
 RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax,
                        OctWalk& w, const LdsTopI32* top = nullptr) {
     if (m.n_nodes == 0) return false;
@@ -680,6 +685,7 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
     w.bt = 0.0;
     w.nlf = w.nle = 0;
     w.ndone = 0;
+    w.enter = 0;
     w.cur = m.node_base;
     w.depth = 0;
     w.path = 0;
@@ -714,12 +720,12 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
         w.mn[k] = m.root_box[k];
         w.mx[k] = m.root_box[3 + k];
     }
-#if RT_WALK_TIGHT
-    (void)top;
-    walk_enter_mask(ray, inv, w, (uint32_t)m.root_exist);
-#else
-    walk_enter(sc, ray, inv, w, top);
-#endif
+    if constexpr (Slots) {
+        (void)top;
+        w.enter = 1;  // the first step enters the root (walk_node_slots)
+    } else {
+        walk_enter(sc, ray, inv, w, top);
+    }
     return true;
 }
 
@@ -844,6 +850,11 @@ constexpr int kSlotAncLevels = 9;
 RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w,
                            LdsTopI32* anc = nullptr) {
     RT_DBG_TSTART(t_pop);
+    uint32_t exist = 0;  // a node to enter: its existence mask (the root at a walk's start, or a descent)
+    if (w.enter) {
+        w.enter = 0;
+        exist = (uint32_t)m.root_exist;
+    } else {
     if (w.pm == 0) {  // `cur` exhausted: resume at the nearest ancestor with children left
         int lv = w.depth;
         uint32_t pm = 0;
@@ -943,8 +954,10 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
         const double cc = (w.mn[k] + w.mx[k]) / 2.0;
         if ((oi >> (2 - k)) & 1u) w.mn[k] = cc; else w.mx[k] = cc;
     }
-    walk_enter_mask(ray, inv, w, slot_exist(c));
+    exist = slot_exist(c);
     RT_DBG_TEND(14, t_pick);
+    }
+    walk_enter_mask(ray, inv, w, exist);  // one octant_mask for the descents and the walks' starts
     return WALK_RUN;
 }
 RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w,

@@ -75,7 +75,8 @@ RT_DEV void park_store(const Park& p, const WalkRegs& r) {
     for (int k = 0; k < 3; ++k) { p.D(9 + k) = r.w.mn[k]; p.D(12 + k) = r.w.mx[k]; }
     p.D(15) = r.w.bt;
     p.D(16) = r.wt;
-    p.I(0) = r.w.cur; p.I(1) = r.w.depth | (int32_t)(r.w.ndone << 24); p.I(2) = (int32_t)r.w.path; p.I(3) = (int32_t)r.w.pm;
+    p.I(0) = r.w.cur; p.I(1) = r.w.depth | (int32_t)(r.w.ndone << 24) | (int32_t)(r.w.enter << 25); p.I(2) = (int32_t)r.w.path;
+    p.I(3) = (int32_t)r.w.pm;
     p.I(4) = (int32_t)(uint32_t)r.w.stk; p.I(5) = (int32_t)(uint32_t)(r.w.stk >> 32); p.I(6) = (int32_t)r.w.stk8;
     p.I(7) = (int32_t)r.w.order; p.I(8) = r.w.lpos; p.I(9) = r.w.lend; p.I(10) = r.w.best;
     p.I(11) = r.hobj; p.I(12) = r.hprim; p.I(13) = r.g; p.I(14) = r.mi; p.I(15) = r.occluded;
@@ -88,7 +89,8 @@ RT_DEV void park_load(const Park& p, WalkRegs& r) {
     for (int k = 0; k < 3; ++k) { r.w.mn[k] = p.D(9 + k); r.w.mx[k] = p.D(12 + k); }
     r.w.bt = p.D(15);
     r.wt = p.D(16);
-    r.w.cur = p.I(0); r.w.depth = p.I(1) & 0xFF; r.w.ndone = (uint32_t)p.I(1) >> 24; r.w.path = (uint32_t)p.I(2);
+    r.w.cur = p.I(0); r.w.depth = p.I(1) & 0xFF; r.w.ndone = ((uint32_t)p.I(1) >> 24) & 1u;
+    r.w.enter = ((uint32_t)p.I(1) >> 25) & 1u; r.w.path = (uint32_t)p.I(2);
     r.w.pm = (uint32_t)p.I(3);
     r.w.stk = (uint64_t)(uint32_t)p.I(4) | ((uint64_t)(uint32_t)p.I(5) << 32); r.w.stk8 = (uint32_t)p.I(6);
     r.w.order = (uint32_t)p.I(7); r.w.lpos = p.I(8); r.w.lend = p.I(9); r.w.best = p.I(10);
@@ -288,7 +290,7 @@ RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
     p.D(12) = r.w.bt;
     p.D(13) = r.wt;
     p.I(0) = r.w.cur;
-    p.I(1) = (int32_t)((uint32_t)r.w.depth | (r.w.pm << 8) | (r.w.stk8 << 16) | (r.w.ndone << 24));
+    p.I(1) = (int32_t)((uint32_t)r.w.depth | (r.w.pm << 8) | (r.w.stk8 << 16) | (r.w.ndone << 24) | (r.w.enter << 25));
     p.I(2) = (int32_t)r.w.path;
     p.I(3) = (int32_t)(uint32_t)r.w.stk; p.I(4) = (int32_t)(uint32_t)(r.w.stk >> 32);
     p.I(5) = (int32_t)r.w.order; p.I(6) = r.w.lpos; p.I(7) = r.w.lend; p.I(8) = r.w.best;
@@ -307,7 +309,8 @@ RT_DEV void park2_load(const Park& p, WalkRegs& r) {
     r.wt = p.D(13);
     r.w.cur = p.I(0);
     const uint32_t dps = (uint32_t)p.I(1);
-    r.w.depth = (int32_t)(dps & 0xFFu); r.w.pm = (dps >> 8) & 0xFFu; r.w.stk8 = (dps >> 16) & 0xFFu; r.w.ndone = dps >> 24;
+    r.w.depth = (int32_t)(dps & 0xFFu); r.w.pm = (dps >> 8) & 0xFFu; r.w.stk8 = (dps >> 16) & 0xFFu;
+    r.w.ndone = (dps >> 24) & 1u; r.w.enter = (dps >> 25) & 1u;
     r.w.path = (uint32_t)p.I(2);
     r.w.stk = (uint64_t)(uint32_t)p.I(3) | ((uint64_t)(uint32_t)p.I(4) << 32);
     r.w.order = (uint32_t)p.I(5); r.w.lpos = p.I(6); r.w.lend = p.I(7); r.w.best = p.I(8);
@@ -364,7 +367,9 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
                 const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
                 fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, top);
                 RT_DBG_TEND(15, t_bg);
-            } else {
+            }
+            // (a walk begun above takes its first step right away: the slot walk enters the root there)
+            if (!fin && r.w.cur >= 0) {
                 double t;
                 int prim;
                 const int st = walk_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim, r.mi == sc.top_mesh ? top : nullptr,

@@ -229,7 +229,7 @@ struct ClosestQuery {
     RT_DEV bool next_mesh() {
         for (++g; g < tables(sc)->n_gen; ++g) {
             const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
-            if (o.geom == GEOM_MESH && walk_begin(sc, sc.meshes[o.mesh], ray, inv, h.obj >= 0 ? h.t : INFINITY, w))
+            if (o.geom == GEOM_MESH && walk_begin<false>(sc, sc.meshes[o.mesh], ray, inv, h.obj >= 0 ? h.t : INFINITY, w))
                 return true;
         }
         return false;
@@ -281,7 +281,7 @@ struct ShadowQuery {
     RT_DEV bool next_mesh() {
         for (++g; g < tables(sc)->n_gen; ++g) {
             const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
-            if (o.geom == GEOM_MESH && walk_begin(sc, sc.meshes[o.mesh], ray, inv, dist, w)) return true;
+            if (o.geom == GEOM_MESH && walk_begin<false>(sc, sc.meshes[o.mesh], ray, inv, dist, w)) return true;
         }
         return false;
     }
