@@ -140,7 +140,9 @@ constexpr int kMaxCompactObjects = 16;  // compact scenes also hold their object
 // v_readlane instructions in the cornell megakernel).
 struct CompactTab {
     int32_t n_ax[3];                         // planes with n = +-e_k, per axis k
-    int32_t n_sph, n_gen, pad;
+    int32_t n_sph, n_gen;
+    int32_t last_mesh_g;                     // the last gen_idx slot holding a mesh (-1 none): a walk pool
+                                             // query whose walk of that mesh ended has its result
     int32_t ax_idx[3][kMaxAxisPlanes];
     double ax_pos[3][kMaxAxisPlanes];        // plane point coordinate along its axis
     int32_t sph_idx[kMaxSpheres];

@@ -274,7 +274,10 @@ struct WalkPool {
     uint8_t* status;    // LDS [256] per owner column: 0 closest query, 1 shadow query, 2 done
 };
 enum : uint8_t { POOL_CLOSEST = 0, POOL_SHADOW = 1, POOL_DONE = 2 };
-constexpr int kPoolRefill = 8;  // refill only when at least this many lanes of the round are idle
+#ifndef RT_POOL_REFILL
+#define RT_POOL_REFILL 16
+#endif
+constexpr int kPoolRefill = RT_POOL_REFILL;  // refill only when at least this many lanes of the round are idle
 
 // Compact park of the walk pool (fits 3 blocks of 256 threads per CU, i.e. 3 waves/SIMD): no 1/d
 // (recomputed by make_inv when a query is loaded: the same bits), no NEE term (the owner keeps it in
@@ -388,6 +391,7 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
                         fin = r.occluded;
                     }
                     r.w.cur = -1;  // next step: the next mesh, if any
+                    fin |= r.g >= tables(sc)->last_mesh_g;  // none: the query's result is complete now
                 }
             }
             if (fin) {  // results for the owner's vertex phase, then the status word

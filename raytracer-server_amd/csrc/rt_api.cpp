@@ -544,6 +544,9 @@ void fill_compact(const Packed& p, rt::CompactTab* ds, int32_t* compact) {
     for (int k = 0; k < 3; ++k) ds->n_ax[k] = ok ? nax[k] : 0;
     ds->n_sph = ok ? ns : 0;
     ds->n_gen = ok ? ng : 0;
+    ds->last_mesh_g = -1;
+    for (int g = 0; g < ds->n_gen; ++g)
+        if (p.objects[ds->gen_idx[g]].geom == rt::GEOM_MESH) ds->last_mesh_g = g;
 }
 
 // f32 perf-mode tables (scene_layout.h: Obj32 / Bvh32 / Tri32). BVH boxes are rounded outward and
