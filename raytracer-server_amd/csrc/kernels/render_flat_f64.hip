@@ -521,11 +521,20 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
     }
     // per lane (one column per thread): subpixel accumulator; the closest-hit query ray (o, d), the
     // shadow query ray (o, d, |y - x|); results per (mesh, lane); queries outstanding per lane
+    // The closest-hit and the shadow query of a lane are issued in the same iteration from the same
+    // point (the shadow ray's x and the next ray's origin, integrator_f64.h shade_vertex; a camera ray
+    // never coexists with a shadow query: the path waits for it, `endwait`), so they share one origin
+    // column: s_qo origin, s_qdc closest direction, s_qds shadow direction + |y - x|. Closest results:
+    // t, and the hit triangle as its index within the mesh (flat meshes hold <= kFlatMaxTris). The
+    // mirror-bounce state (o, pre-bounce throughput) lives in LDS as in k_megakernel_f64 (LdsCold):
+    // 12 VGPRs less at 3 waves/SIMD.
     __shared__ double s_acc[3 * kBlk];
-    __shared__ double s_qc[6 * kBlk], s_qs[7 * kBlk];
+    __shared__ double s_qo[3 * kBlk], s_qdc[3 * kBlk], s_qds[4 * kBlk];
     __shared__ double s_rt[kFlatMeshes * kBlk];
-    __shared__ int32_t s_rp[kFlatMeshes * kBlk];
+    __shared__ uint8_t s_rp[kFlatMeshes * kBlk];
     __shared__ uint8_t s_ro[kFlatMeshes * kBlk];
+    __shared__ double s_cold[6 * kBlk];
+    const LdsCold cold{(LdsD*)s_cold + threadIdx.x};
     __shared__ int32_t s_pend[kBlk];
     // per mesh: queued queries, entry = lane (closest hit) or 256 + lane (shadow)
     __shared__ int32_t s_ring[kFlatMeshes][kFpRing];
@@ -575,18 +584,19 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                 RT_DBG_WAVE(12, e >= 0);
                 if (e >= 0) {
                     const int kind = e >> 8, who = e & (kBlk - 1);
-                    const LdsD* q = kind ? (const LdsD*)s_qs : (const LdsD*)s_qc;
-                    const Ray r{v3(q[who], q[kBlk + who], q[2 * kBlk + who]),
-                                v3(q[3 * kBlk + who], q[4 * kBlk + who], q[5 * kBlk + who])};
+                    const LdsD* qo = (const LdsD*)s_qo;
+                    const LdsD* q = kind ? (const LdsD*)s_qds : (const LdsD*)s_qdc;
+                    const Ray r{v3(qo[who], qo[kBlk + who], qo[2 * kBlk + who]),
+                                v3(q[who], q[kBlk + who], q[2 * kBlk + who])};
                     const RayInv inv = make_inv(r.d);
                     double t = 0.0;
                     int prim = -1;
                     const bool hit = flat_query(sc, m, r, inv, &t, &prim);
                     if (kind == 0) {
                         s_rt[m * kBlk + who] = t;
-                        s_rp[m * kBlk + who] = hit ? prim : -1;
+                        s_rp[m * kBlk + who] = hit ? (uint8_t)(prim - sc.meshes[m].tri_base) : (uint8_t)0xFF;
                     } else {
-                        s_ro[m * kBlk + who] = hit && !(t + 0.001 >= q[6 * kBlk + who]) ? 1 : 0;
+                        s_ro[m * kBlk + who] = hit && !(t + 0.001 >= q[3 * kBlk + who]) ? 1 : 0;
                     }
                     const int32_t left = __hip_atomic_fetch_sub(&s_pend[who], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if (RT_QCHECK && left <= 0) RT_QFAIL(2);
@@ -619,13 +629,13 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                     const DevObject& o = sc.objects[idx];
                     if (o.geom == GEOM_MESH && ((qmask >> o.mesh) & 1u)) {
                         const int p = s_rp[o.mesh * kBlk + tid];
-                        if (p >= 0) consider(h, s_rt[o.mesh * kBlk + tid], idx, p);
+                        if (p != 0xFF) consider(h, s_rt[o.mesh * kBlk + tid], idx, sc.meshes[o.mesh].tri_base + p);
                     }
                 }
                 nverts += h.obj >= 0;
                 ShadowDefer df;
                 df.pending = false;
-                const bool cont = shade_vertex<C>(sc, a, ps, h, &df);
+                const bool cont = shade_vertex<C, LdsCold>(sc, a, ps, h, &df, cold);
                 traced = false;
                 if (df.pending) {  // the analytic objects let the shadow ray through; a mesh may block it
                     shadow_q = true;
@@ -650,9 +660,9 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                 if (near_box(M.cull_box, sr, sinv, M.cull_pad, dist)) want_s |= 1u << m;
             }
             if (want_s) {
-                s_qs[tid] = sr.o.x; s_qs[kBlk + tid] = sr.o.y; s_qs[2 * kBlk + tid] = sr.o.z;
-                s_qs[3 * kBlk + tid] = sr.d.x; s_qs[4 * kBlk + tid] = sr.d.y; s_qs[5 * kBlk + tid] = sr.d.z;
-                s_qs[6 * kBlk + tid] = dist;
+                s_qo[tid] = sr.o.x; s_qo[kBlk + tid] = sr.o.y; s_qo[2 * kBlk + tid] = sr.o.z;
+                s_qds[tid] = sr.d.x; s_qds[kBlk + tid] = sr.d.y; s_qds[2 * kBlk + tid] = sr.d.z;
+                s_qds[3 * kBlk + tid] = dist;
                 spend = true;
                 smask = want_s;
             } else {  // no mesh near the shadow segment: unblocked now
@@ -718,8 +728,8 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                 if (near_box(M.cull_box, ps.ray, inv, M.cull_pad, tmax)) want_c |= 1u << m;
             }
             if (want_c) {
-                s_qc[tid] = ps.ray.o.x; s_qc[kBlk + tid] = ps.ray.o.y; s_qc[2 * kBlk + tid] = ps.ray.o.z;
-                s_qc[3 * kBlk + tid] = ps.ray.d.x; s_qc[4 * kBlk + tid] = ps.ray.d.y; s_qc[5 * kBlk + tid] = ps.ray.d.z;
+                s_qo[tid] = ps.ray.o.x; s_qo[kBlk + tid] = ps.ray.o.y; s_qo[2 * kBlk + tid] = ps.ray.o.z;
+                s_qdc[tid] = ps.ray.d.x; s_qdc[kBlk + tid] = ps.ray.d.y; s_qdc[2 * kBlk + tid] = ps.ray.d.z;
             }
             qmask = want_c;
             traced = true;

@@ -275,7 +275,7 @@ struct WalkPool {
 };
 enum : uint8_t { POOL_CLOSEST = 0, POOL_SHADOW = 1, POOL_DONE = 2 };
 #ifndef RT_POOL_REFILL
-#define RT_POOL_REFILL 16
+#define RT_POOL_REFILL 32
 #endif
 constexpr int kPoolRefill = RT_POOL_REFILL;  // refill only when at least this many lanes of the round are idle
 
