@@ -113,6 +113,7 @@ struct ShadowDefer {
     bool pending;
     V3 o, d, c;
     double dist;
+    uint32_t meshes;  // the meshes near the shadow segment (mesh_near_mask): the ones that could block it
 };
 
 // Where a path keeps the two values only a mirror bounce hands on to the next vertex (read there only
@@ -221,8 +222,10 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
                     // mutually_visible (scene.rs:258-270) split: analytic objects now, meshes deferred
                     const RayInv inv = make_inv(sr.d);
                     vis = visible_analytic<C>(sc, y, sr, inv, dist) ? 1. : 0.;
-                    if (vis > 0. && mesh_candidate<C>(sc, sr, inv, dist)) {
+                    const uint32_t near = vis > 0. ? mesh_near_mask<C>(sc, sr, inv, dist) : 0u;
+                    if (near) {
                         defer->pending = true;
+                        defer->meshes = near;
                         defer->o = sr.o;
                         defer->d = sr.d;
                         defer->dist = dist;

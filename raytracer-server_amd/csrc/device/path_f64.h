@@ -1433,19 +1433,24 @@ RT_DEV void trace_meshes(const DevScene& sc, const Ray& ray, const RayInv& inv, 
         if (mesh_hit(sc, sc.meshes[o.mesh], ray, inv, h.obj >= 0 ? h.t : INFINITY, &t, &prim)) consider(h, t, idx, prim);
     }
 }
-// Could any mesh change this ray's result (closest hit so far at tmax / shadow distance tmax)?
+// Which meshes could change this ray's result (closest hit so far at tmax / shadow distance tmax)?
+// Bit m: mesh m (non-empty octree) passes near_box against its cull box.
 template <class C>
-RT_DEV bool mesh_candidate(const DevScene& sc, const Ray& ray, const RayInv& inv, double tmax) {
+RT_DEV uint32_t mesh_near_mask(const DevScene& sc, const Ray& ray, const RayInv& inv, double tmax) {
     CTab* T = tables(sc);
-    bool any = false;
+    uint32_t mask = 0;
     for (int i = 0; i < T->n_gen; ++i) {
         const DevObject& o = sc.objects[T->gen_idx[i]];
         if (o.geom == GEOM_MESH && sc.meshes[o.mesh].n_nodes > 0) {
             const DevMesh& m = sc.meshes[o.mesh];
-            any |= near_box(m.cull_box, ray, inv, m.cull_pad, tmax);
+            mask |= near_box(m.cull_box, ray, inv, m.cull_pad, tmax) ? 1u << o.mesh : 0u;
         }
     }
-    return any;
+    return mask;
+}
+template <class C>
+RT_DEV bool mesh_candidate(const DevScene& sc, const Ray& ray, const RayInv& inv, double tmax) {
+    return mesh_near_mask<C>(sc, ray, inv, tmax) != 0;
 }
 // mutually_visible split: the analytic objects here, the meshes later (mesh_occludes).
 template <class C>

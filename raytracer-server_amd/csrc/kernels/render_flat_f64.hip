@@ -592,6 +592,8 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                     double t = 0.0;
                     int prim = -1;
                     const bool hit = flat_query(sc, m, r, inv, &t, &prim);
+                    RT_DBG(0);           // diagnostic builds: queries evaluated ...
+                    if (hit) RT_DBG(1);  // ... and those with a triangle hit
                     if (kind == 0) {
                         s_rt[m * kBlk + who] = t;
                         s_rp[m * kBlk + who] = hit ? (uint8_t)(prim - sc.meshes[m].tri_base) : (uint8_t)0xFF;
@@ -611,6 +613,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
         bool finish = false, shadow_q = false;
         Ray sr{v3(0, 0, 0), v3(0, 0, 1)};
         double dist = 0.0;
+        uint32_t near_s = 0;
         if (ready) {
             if (spend) {  // the last vertex's NEE term, unless a mesh blocks its shadow ray (mutually_visible)
                 bool occluded = false;
@@ -642,6 +645,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                     pc = df.c;
                     dist = df.dist;
                     sr = Ray{df.o, df.d};
+                    near_s = df.meshes;
                 }
                 if (!cont) {
                     if (shadow_q) endwait = true;
@@ -654,11 +658,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
         // shadow queries of this vertex, per mesh near the segment
         uint32_t want_s = 0;
         if (shadow_q) {
-            const RayInv sinv = make_inv(sr.d);
-            for (int m = 0; m < nm; ++m) {
-                const DevMesh& M = sc.meshes[m];
-                if (near_box(M.cull_box, sr, sinv, M.cull_pad, dist)) want_s |= 1u << m;
-            }
+            want_s = near_s;  // shade_vertex's mesh_near_mask of the segment (non-zero: df.pending)
             if (want_s) {
                 s_qo[tid] = sr.o.x; s_qo[kBlk + tid] = sr.o.y; s_qo[2 * kBlk + tid] = sr.o.z;
                 s_qds[tid] = sr.d.x; s_qds[kBlk + tid] = sr.d.y; s_qds[2 * kBlk + tid] = sr.d.z;
