@@ -675,11 +675,12 @@ RT_DEV void walk_reload_ahead(const DevScene& sc, OctWalk& w, const LdsTopI32* t
 // Slots: the walk continues with walk_step<true> (the slot walk: the root is entered in its first step),
 // or with walk_step<false> (the node_kids walk: entered here).
 template <bool Slots = (RT_WALK_TIGHT != 0)>
+// cull = false: the caller already knows the ray passes near_box for this mesh (mesh_near_mask).
 RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax,
-                       OctWalk& w, const LdsTopI32* top = nullptr) {
+                       OctWalk& w, const LdsTopI32* top = nullptr, bool cull = true) {
     if (m.n_nodes == 0) return false;
     RT_DBG(0);
-    if (!near_box(m.cull_box, ray, inv, m.cull_pad, tmax)) return false;
+    if (cull && !near_box(m.cull_box, ray, inv, m.cull_pad, tmax)) return false;
     RT_DBG(1);
     w.best = -1;
     w.bt = 0.0;

@@ -37,6 +37,21 @@ RT_DEV bool next_mesh_walk(const DevScene& sc, const Ray& r, const RayInv& inv, 
     }
     return false;
 }
+// The walk pool's form: `near` = the meshes the query's owner found near the ray (mesh_near_mask, same
+// tmax), so only those are begun, without repeating their near_box test.
+template <class C>
+RT_DEV bool next_mesh_walk_near(const DevScene& sc, const Ray& r, const RayInv& inv, double tmax, int& g, int& mi,
+                                OctWalk& w, uint32_t near, const LdsTopI32* top = nullptr) {
+    for (++g; g < tables(sc)->n_gen; ++g) {
+        const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
+        if (o.geom == GEOM_MESH && ((near >> o.mesh) & 1u) &&
+            walk_begin(sc, sc.meshes[o.mesh], r, inv, tmax, w, o.mesh == sc.top_mesh ? top : nullptr, false)) {
+            mi = o.mesh;
+            return true;
+        }
+    }
+    return false;
+}
 
 // Megakernel for scenes with triangle meshes: octree walks interleaved with path vertices.
 // A walk is long-tailed (tens of steps for the few rays that reach the mesh's box; none for the
@@ -284,8 +299,8 @@ constexpr int kPoolRefill = RT_POOL_REFILL;  // refill only when at least this m
 // registers), depth / pm / stk8 packed in one word. Doubles: ray o, d; box mn, mx; walk best t;
 // query t (closest hit so far / shadow distance). Ints: cur, depth | pm << 8 | stk8 << 16, path,
 // stk (2 words), order, lpos, lend, best, hit object, hit prim, gen slot, mesh, occluded.
-constexpr int kPark2D = 14, kPark2I = RT_WALK_READAHEAD ? 17 : 16;
-enum : int { P2_T = 13, P2_HOBJ = 9, P2_HPRIM = 10, P2_OCC = 13 };
+constexpr int kPark2D = 14, kPark2I = RT_WALK_READAHEAD ? 18 : 17;
+enum : int { P2_T = 13, P2_HOBJ = 9, P2_HPRIM = 10, P2_OCC = 13, P2_NEAR = 16 };
 RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
     p.D(0) = r.wr.o.x; p.D(1) = r.wr.o.y; p.D(2) = r.wr.o.z;
     p.D(3) = r.wr.d.x; p.D(4) = r.wr.d.y; p.D(5) = r.wr.d.z;
@@ -300,7 +315,7 @@ RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
     p.I(9) = r.hobj; p.I(10) = r.hprim; p.I(11) = r.g; p.I(12) = r.mi; p.I(13) = r.occluded;
     p.I(14) = r.w.nlf; p.I(15) = r.w.nle;
 #if RT_WALK_READAHEAD
-    p.I(16) = r.w.nc;
+    p.I(17) = r.w.nc;
 #endif
 }
 RT_DEV void park2_load(const Park& p, WalkRegs& r) {
@@ -320,20 +335,21 @@ RT_DEV void park2_load(const Park& p, WalkRegs& r) {
     r.hobj = p.I(9); r.hprim = p.I(10); r.g = p.I(11); r.mi = p.I(12); r.occluded = p.I(13);
     r.w.nlf = p.I(14); r.w.nle = p.I(15);
 #if RT_WALK_READAHEAD
-    r.w.nc = p.I(16);  // its child entries are loaded again by walk_reload_ahead
+    r.w.nc = p.I(17);  // its child entries are loaded again by walk_reload_ahead
 #else
     r.w.nc = kNcNone;
 #endif
 }
-// A new pool query (see park_query).
-RT_DEV void park2_query(const Park& p, const Ray& r, double wt, int32_t hobj, int32_t hprim) {
+// A new pool query (see park_query); near: the meshes near the ray (mesh_near_mask).
+RT_DEV void park2_query(const Park& p, const Ray& r, double wt, int32_t hobj, int32_t hprim, uint32_t near) {
+    p.I(P2_NEAR) = (int32_t)near;
     p.D(0) = r.o.x; p.D(1) = r.o.y; p.D(2) = r.o.z;
     p.D(3) = r.d.x; p.D(4) = r.d.y; p.D(5) = r.d.z;
     p.D(13) = wt;
     p.I(0) = -1;
     p.I(9) = hobj; p.I(10) = hprim; p.I(11) = -1; p.I(13) = 0;
 #if RT_WALK_READAHEAD
-    p.I(16) = kNcNone;
+    p.I(17) = kNcNone;
 #endif
 }
 
@@ -368,7 +384,7 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
             if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
                 RT_DBG_TSTART(t_bg);
                 const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
-                fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, top);
+                fin = !next_mesh_walk_near<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, (uint32_t)col(q).I(P2_NEAR), top);
                 RT_DBG_TEND(15, t_bg);
             }
             // (a walk begun above takes its first step right away: the slot walk enters the root there)
@@ -543,10 +559,11 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                 RT_DBG_TSTART(t_ta);
                 const RayInv wi = make_inv(ps.ray.d);
                 h = trace_analytic<C>(sc, ps.ray, wi);
-                const bool cand = mesh_candidate<C>(sc, ps.ray, wi, h.obj >= 0 ? h.t : INFINITY);
+                const uint32_t near = mesh_near_mask<C>(sc, ps.ray, wi, h.obj >= 0 ? h.t : INFINITY);
+                const bool cand = near != 0;
                 RT_DBG_TEND(6, t_ta);
                 if (cand) {
-                    if constexpr (P) park2_query(park, ps.ray, h.t, h.obj, h.prim);
+                    if constexpr (P) park2_query(park, ps.ray, h.t, h.obj, h.prim, near);
                     else park_query(park, ps.ray, wi, h.t, h.obj, h.prim);
                     if constexpr (P) s_status[threadIdx.x] = POOL_CLOSEST;
                     phase = PH_WALK_CLOSEST;
@@ -566,7 +583,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                 if (df.pending) {  // shade_vertex found a mesh that could block the shadow ray
                     const Ray sr{df.o, df.d};
                     if constexpr (P) {
-                        park2_query(park, sr, df.dist, -1, -1);
+                        park2_query(park, sr, df.dist, -1, -1, df.meshes);
                         pc = df.c;
                     } else {
                         park_query(park, sr, make_inv(sr.d), df.dist, -1, -1);
