@@ -114,6 +114,7 @@ struct ShadowDefer {
     V3 o, d, c;
     double dist;
     uint32_t meshes;  // the meshes near the shadow segment (mesh_near_mask): the ones that could block it
+    RayInv inv;       // make_inv(d), for the deferred query
 };
 
 // Where a path keeps the two values only a mirror bounce hands on to the next vertex (read there only
@@ -226,6 +227,7 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
                     if (near) {
                         defer->pending = true;
                         defer->meshes = near;
+                        defer->inv = inv;
                         defer->o = sr.o;
                         defer->d = sr.d;
                         defer->dist = dist;

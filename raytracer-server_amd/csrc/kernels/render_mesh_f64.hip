@@ -299,7 +299,10 @@ constexpr int kPoolRefill = RT_POOL_REFILL;  // refill only when at least this m
 // registers), depth / pm / stk8 packed in one word. Doubles: ray o, d; box mn, mx; walk best t;
 // query t (closest hit so far / shadow distance). Ints: cur, depth | pm << 8 | stk8 << 16, path,
 // stk (2 words), order, lpos, lend, best, hit object, hit prim, gen slot, mesh, occluded.
-constexpr int kPark2D = 14, kPark2I = RT_WALK_READAHEAD ? 18 : 17;
+#ifndef RT_PARK_INV
+#define RT_PARK_INV 1  // A/B: the park keeps 1/d (1) or park2_load recomputes it (0)
+#endif
+constexpr int kPark2D = RT_PARK_INV ? 17 : 14, kPark2I = RT_WALK_READAHEAD ? 18 : 17;
 enum : int { P2_T = 13, P2_HOBJ = 9, P2_HPRIM = 10, P2_OCC = 13, P2_NEAR = 16 };
 RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
     p.D(0) = r.wr.o.x; p.D(1) = r.wr.o.y; p.D(2) = r.wr.o.z;
@@ -307,6 +310,9 @@ RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
     for (int k = 0; k < 3; ++k) { p.D(6 + k) = r.w.mn[k]; p.D(9 + k) = r.w.mx[k]; }
     p.D(12) = r.w.bt;
     p.D(13) = r.wt;
+#if RT_PARK_INV
+    p.D(14) = r.wi.rx; p.D(15) = r.wi.ry; p.D(16) = r.wi.rz;
+#endif
     p.I(0) = r.w.cur;
     p.I(1) = (int32_t)((uint32_t)r.w.depth | (r.w.pm << 8) | (r.w.stk8 << 16) | (r.w.ndone << 24) | (r.w.enter << 25));
     p.I(2) = (int32_t)r.w.path;
@@ -321,7 +327,11 @@ RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
 RT_DEV void park2_load(const Park& p, WalkRegs& r) {
     r.wr.o = v3(p.D(0), p.D(1), p.D(2));
     r.wr.d = v3(p.D(3), p.D(4), p.D(5));
+#if RT_PARK_INV
+    r.wi.rx = p.D(14); r.wi.ry = p.D(15); r.wi.rz = p.D(16);
+#else
     r.wi = make_inv(r.wr.d);
+#endif
     for (int k = 0; k < 3; ++k) { r.w.mn[k] = p.D(6 + k); r.w.mx[k] = p.D(9 + k); }
     r.w.bt = p.D(12);
     r.wt = p.D(13);
@@ -341,8 +351,14 @@ RT_DEV void park2_load(const Park& p, WalkRegs& r) {
 #endif
 }
 // A new pool query (see park_query); near: the meshes near the ray (mesh_near_mask).
-RT_DEV void park2_query(const Park& p, const Ray& r, double wt, int32_t hobj, int32_t hprim, uint32_t near) {
+RT_DEV void park2_query(const Park& p, const Ray& r, const RayInv& wi, double wt, int32_t hobj, int32_t hprim,
+                        uint32_t near) {
     p.I(P2_NEAR) = (int32_t)near;
+#if RT_PARK_INV
+    p.D(14) = wi.rx; p.D(15) = wi.ry; p.D(16) = wi.rz;
+#else
+    (void)wi;
+#endif
     p.D(0) = r.o.x; p.D(1) = r.o.y; p.D(2) = r.o.z;
     p.D(3) = r.d.x; p.D(4) = r.d.y; p.D(5) = r.d.z;
     p.D(13) = wt;
@@ -563,7 +579,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                 const bool cand = near != 0;
                 RT_DBG_TEND(6, t_ta);
                 if (cand) {
-                    if constexpr (P) park2_query(park, ps.ray, h.t, h.obj, h.prim, near);
+                    if constexpr (P) park2_query(park, ps.ray, wi, h.t, h.obj, h.prim, near);
                     else park_query(park, ps.ray, wi, h.t, h.obj, h.prim);
                     if constexpr (P) s_status[threadIdx.x] = POOL_CLOSEST;
                     phase = PH_WALK_CLOSEST;
@@ -583,7 +599,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                 if (df.pending) {  // shade_vertex found a mesh that could block the shadow ray
                     const Ray sr{df.o, df.d};
                     if constexpr (P) {
-                        park2_query(park, sr, df.dist, -1, -1, df.meshes);
+                        park2_query(park, sr, df.inv, df.dist, -1, -1, df.meshes);
                         pc = df.c;
                     } else {
                         park_query(park, sr, make_inv(sr.d), df.dist, -1, -1);
