@@ -1434,8 +1434,37 @@ RT_DEV void trace_meshes(const DevScene& sc, const Ray& ray, const RayInv& inv, 
         if (mesh_hit(sc, sc.meshes[o.mesh], ray, inv, h.obj >= 0 ? h.t : INFINITY, &t, &prim)) consider(h, t, idx, prim);
     }
 }
+// near_box's cull in single precision, padded so that it passes every ray near_box passes (a cull may
+// only let more rays through: a mesh walk or query for a ray it could have skipped returns the
+// reference's result anyway). The ray is rounded to f32 (|o32 - o| <= 2^-24 |o|, |d32 - d| <= 2^-24
+// for |d| = 1) and the slab arithmetic adds a few f32 roundings; within the distances where the ray
+// can meet the box (t <= |o| + 4 S for a box inside [-S, S]^3) all of it moves the ray's points by less
+// than 2^-21 (|o| + S). The box is padded by pad = 2^-16 (max |o_k| + S), 16x that (and 30x the f64
+// test's own 1e-7 S pad), and the interval ends are compared with the same slack.
+RT_DEV bool near_mesh32(const DevMesh& m, const Ray& ray, double tmax) {
+    const float o[3] = {(float)ray.o.x, (float)ray.o.y, (float)ray.o.z};
+    const float d[3] = {(float)ray.d.x, (float)ray.d.y, (float)ray.d.z};
+    const float pad = 0x1p-16f * (fmaxf(fabsf(o[0]), fmaxf(fabsf(o[1]), fabsf(o[2]))) + m.cull32_s);
+    float t0 = 0.0f, t1 = INFINITY;
+    bool keep = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float lo = m.cull32[k] - pad, hi = m.cull32[3 + k] + pad;
+        const bool tiny = !(fabsf(d[k]) >= 0x1p-60f);  // (nearly) parallel slab (or NaN): origin inside it
+        keep &= !tiny || !(o[k] < lo || o[k] > hi);
+        const float rc = __builtin_amdgcn_rcpf(d[k]);
+        const float ta = (lo - o[k]) * rc, tb = (hi - o[k]) * rc;
+        t0 = tiny ? t0 : fmaxf(t0, fminf(ta, tb));
+        t1 = tiny ? t1 : fminf(t1, fmaxf(ta, tb));
+    }
+    const float tm = (float)tmax;
+    return keep && !(t0 > t1 + 0x1p-16f * fabsf(t1) + pad) && !(t0 > tm + 0x1p-16f * tm + pad);
+}
+#ifndef RT_NEAR32
+#define RT_NEAR32 1  // A/B: the meshes' near test in f32 (near_mesh32) or f64 (near_box)
+#endif
 // Which meshes could change this ray's result (closest hit so far at tmax / shadow distance tmax)?
-// Bit m: mesh m (non-empty octree) passes near_box against its cull box.
+// Bit m: mesh m (non-empty octree) passes the near test against its cull box.
 template <class C>
 RT_DEV uint32_t mesh_near_mask(const DevScene& sc, const Ray& ray, const RayInv& inv, double tmax) {
     CTab* T = tables(sc);
@@ -1444,7 +1473,12 @@ RT_DEV uint32_t mesh_near_mask(const DevScene& sc, const Ray& ray, const RayInv&
         const DevObject& o = sc.objects[T->gen_idx[i]];
         if (o.geom == GEOM_MESH && sc.meshes[o.mesh].n_nodes > 0) {
             const DevMesh& m = sc.meshes[o.mesh];
+#if RT_NEAR32
+            (void)inv;
+            mask |= near_mesh32(m, ray, tmax) ? 1u << o.mesh : 0u;
+#else
             mask |= near_box(m.cull_box, ray, inv, m.cull_pad, tmax) ? 1u << o.mesh : 0u;
+#endif
         }
     }
     return mask;

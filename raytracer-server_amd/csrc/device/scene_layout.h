@@ -57,6 +57,9 @@ struct alignas(16) DevMesh {
     int32_t root_exist;       // the root's existence mask (KidSlot): the slot walk's first walk_enter
     int32_t pad2;
     double tight_base[3], tight_step;  // KidSlot bounds: base[k] + q * step (cull box min - E, 3 E / 65535)
+    float cull32[6];          // cull_box rounded outward to f32 (near_mesh32's single-precision cull)
+    float cull32_s;           // max(1, |cull box coordinates|): the scale of near_mesh32's padding
+    int32_t pad4;
     // Flat octree (the cubes): the root is a leaf, or a parent whose children are all leaves, with at
     // most kFlatMaxTris triangles and every leaf list in triangle order. flat_leaf[j / 4] byte j % 4 =
     // the leaves (octant bits; bit 0 for a root leaf) that hold triangle j; flat_kids = octants with a

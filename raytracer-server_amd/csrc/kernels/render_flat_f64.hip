@@ -725,7 +725,11 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
             const double tmax = h.obj >= 0 ? h.t : INFINITY;
             for (int m = 0; m < nm; ++m) {
                 const DevMesh& M = sc.meshes[m];
+#if RT_NEAR32
+                if (near_mesh32(M, ps.ray, tmax)) want_c |= 1u << m;
+#else
                 if (near_box(M.cull_box, ps.ray, inv, M.cull_pad, tmax)) want_c |= 1u << m;
+#endif
             }
             if (want_c) {
                 s_qo[tid] = ps.ray.o.x; s_qo[kBlk + tid] = ps.ray.o.y; s_qo[2 * kBlk + tid] = ps.ray.o.z;

@@ -286,6 +286,15 @@ int pack_scene(rt_scene* s) {
             double mx = 1.0;
             for (double v : dm.cull_box) mx = std::fmax(mx, std::fabs(v));
             dm.cull_pad = 1e-7 * mx;
+            // f32 copy rounded outward (path_f64.h near_mesh32)
+            for (int k = 0; k < 3; ++k) {
+                float lo = (float)dm.cull_box[k], hi = (float)dm.cull_box[3 + k];
+                if ((double)lo > dm.cull_box[k]) lo = std::nextafter(lo, -INFINITY);
+                if ((double)hi < dm.cull_box[3 + k]) hi = std::nextafter(hi, INFINITY);
+                dm.cull32[k] = lo;
+                dm.cull32[3 + k] = hi;
+            }
+            dm.cull32_s = (float)mx * (1.0f + 0x1p-20f);
         }
         double cum = 0.0;
         for (size_t t = 0; t < m.num_triangles(); ++t) {
