@@ -233,7 +233,7 @@ int main(int argc, char** argv) {
     T3.after = true; T3.qbits = 8;
     T4.after = true; T4.qbits = 16; T4.qref = &M.bbox;
     Counts base, tight, after, q8, q16;
-    long past = 0;
+    long past = 0, root_dead = 0, miss_walks = 0;
     for (const Ray& r : Q) {
         if (!near(M.bbox, r, pad) && !near(M.oct_bbox, r, pad)) continue;
         ++past;
@@ -245,6 +245,16 @@ int main(int argc, char** argv) {
         walk(M, 0, M.oct_bbox, r, &h3, &t3, after, &T2, pad, rocts);
         walk(M, 0, M.oct_bbox, r, &h3, &t3, q8, &T3, pad, rocts);
         walk(M, 0, M.oct_bbox, r, &h3, &t3, q16, &T4, pad, rocts);
+        {  // would a pre-test of the root children's subtree bounds have rejected this walk?
+            bool any = false;
+            for (int k = 0; k < 8; ++k) {
+                const int ch = M.nodes[0].children[k];
+                if (ch >= 0 && near(T.box[ch], r, pad)) any = true;
+            }
+            root_dead += !any;
+            miss_walks += !a;
+            if (!any && a) { std::fprintf(stderr, "root pre-test rejected a hit\n"); return 2; }
+        }
         base.hits += a;
         tight.hits += b;
         if (a != b || (a && (t1 != t2 || std::memcmp(&h1.t, &h2.t, 8) != 0))) {
@@ -260,6 +270,8 @@ int main(int argc, char** argv) {
     std::printf("%zu queries, %ld walk the octree (nodes %zu)\n", Q.size(), past, M.nodes.size());
     pr("base", base);
     pr("tight", tight);
+    std::printf("walks rejected by the 8 root children's subtree bounds: %.3f (misses %.3f)\n", (double)root_dead / past,
+                (double)miss_walks / past);
     pr("after", after);
     pr("q8", q8);
     pr("q16 mesh", q16);
