@@ -523,6 +523,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     bool nvalid = false;
     int phase = PH_TRACE;
     bool walking = false, cont = false;
+    HitRec hh{0.0, -1, -1};  // pool kernel: the hit this path shades next (walk result or analytic trace)
+    bool has_hit = false;
     RT_DBG_TINIT();
     while (__any(active)) {
         RT_DBG_WAVE(8, lane_id_is0());
@@ -548,6 +550,91 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
         // pool: after a walk round, shade only once pool_vmin paths are ready (denser vertex phases)
         const bool vphase = !P || !took || __popcll(__ballot(active && !walking)) >= pool_vmin;
         RT_DBG_WAVE(9, vphase && active && !walking);
+        if constexpr (P) {
+          // Pool kernel: per iteration a ready path first shades the hit it holds (the closest walk's
+          // result, or its last trace's analytic hit), then traces its next ray (the path going on, or
+          // the unit's next sample): one shade block and one trace block per iteration, and a vertex
+          // whose closest hit needed a walk traces its successor in the same iteration as its shading.
+          if (vphase && active && !walking) {
+            bool sample_end = false;
+            if (phase == PH_WALK_SHADOW) {  // the shadow result (mutually_visible's mesh part)
+                if (!park.I(P2_OCC)) ps.L = ps.L + pc;
+                phase = PH_TRACE;
+                sample_end = !cont;
+            } else if (phase == PH_WALK_CLOSEST) {  // the closest hit: shaded now
+                hh = HitRec{park.D(P2_T), park.I(P2_HOBJ), park.I(P2_HPRIM)};
+                has_hit = true;
+                phase = PH_TRACE;
+            }
+            if (has_hit) {
+                has_hit = false;
+                nverts += hh.obj >= 0;
+                ShadowDefer df;
+                df.pending = false;
+                RT_DBG_TSTART(t_sv);
+                cont = shade_vertex<C>(sc, a, ps, hh, &df);
+                RT_DBG_TEND(8, t_sv);
+                if (df.pending) {  // shade_vertex found a mesh that could block the shadow ray
+                    park2_query(park, Ray{df.o, df.d}, df.inv, df.dist, -1, -1, df.meshes);
+                    pc = df.c;
+                    s_status[threadIdx.x] = POOL_SHADOW;
+                    phase = PH_WALK_SHADOW;
+                    walking = true;
+                } else {
+                    sample_end = !cont;
+                }
+            }
+            if (sample_end) {
+                fresh = true;
+                if (id < a.n_whole) {
+                    V3 acc = v3(acc_l[0], acc_l[256], acc_l[512]);
+                    acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                    acc_l[0] = acc.x; acc_l[256] = acc.y; acc_l[512] = acc.z;
+                    if (++s == a.n_samples) {
+                        double* o = sub_buf + (size_t)id * 3;
+                        o[0] = acc.x;
+                        o[1] = acc.y;
+                        o[2] = acc.z;
+                        if (++id < end) {  // the next subpixel of the run, no ticket
+                            s = 0;
+                            acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
+                            nvalid = false;
+                        } else {
+                            done = true;
+                        }
+                    }
+                } else {  // split tail (k_tail_sum_f64)
+                    double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
+                    o[0] = ps.L.x;
+                    o[1] = ps.L.y;
+                    o[2] = ps.L.z;
+                    done = !unit_has_next(a, id, s);
+                    ++s;
+                }
+            }
+            // the next ray, unless a shadow query is pending or the unit is done (a new ticket first)
+            if (!walking && !done) {
+                if (fresh) {
+                    begin_sample(sc, a, subpixel_of(a, id), s, ps);
+                    fresh = false;
+                }
+                RT_DBG_TSTART(t_ta);
+                const RayInv wi = make_inv(ps.ray.d);
+                const HitRec h = trace_analytic<C>(sc, ps.ray, wi);
+                const uint32_t near = mesh_near_mask<C>(sc, ps.ray, wi, h.obj >= 0 ? h.t : INFINITY);
+                RT_DBG_TEND(6, t_ta);
+                if (near) {
+                    park2_query(park, ps.ray, wi, h.t, h.obj, h.prim, near);
+                    s_status[threadIdx.x] = POOL_CLOSEST;
+                    phase = PH_WALK_CLOSEST;
+                    walking = true;
+                } else {
+                    hh = h;  // shaded in the next iteration
+                    has_hit = true;
+                }
+            }
+          }
+        } else {
         if (vphase && active && !walking) {
             bool shade_now = false, sample_end = false, trace_now = true;
             HitRec h;
@@ -641,6 +728,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                     ++s;
                 }
             }
+        }
         }
         if constexpr (P) queue_put(wp.q, walking && !was_walking, (int32_t)threadIdx.x);
         RT_DBG_TEND(2, t_vx);
