@@ -21,7 +21,7 @@ namespace {
 
 struct Counts {
     long box_tests = 0, descents = 0, leaves = 0, tris = 0, queries = 0, hits = 0;
-    long f32_amb = 0, f32_tests = 0, culled = 0, visits = 0, dead_visits = 0, survivors = 0;
+    long f32_amb = 0, f32_tests = 0, culled = 0, visits = 0, dead_visits = 0, survivors = 0, tri_culled = 0;
 };
 
 struct Tight {
@@ -29,6 +29,7 @@ struct Tight {
     bool after = false;     // test only children whose octant box the ray hits
     int qbits = 0;          // > 0: boxes quantized to qbits per coordinate over the parent box +- its extent
     const BBox* qref = nullptr;  // quantise against this box (the mesh's) instead of the parent's
+    bool tri_cull = false;       // also skip a leaf triangle whose own (quantized) bounds the ray passes far from
 };
 // conservative quantization of child box c inside parent box b's range [b.min - e, b.max + e]
 BBox quant(const BBox& c, const BBox& b, int bits) {
@@ -162,6 +163,18 @@ bool walk(const Mesh& m, int ni, BBox box, const Ray& ray, Hit* h, int* tri, Cou
     bool any = false;
     for (int id : node.tris) {
         Hit hh;
+        if (T && T->tri_cull) {
+            const Tri t = m.tri(id);
+            BBox tb{v3(std::fmin(std::fmin(t.a.x, t.b.x), t.c.x), std::fmin(std::fmin(t.a.y, t.b.y), t.c.y),
+                       std::fmin(std::fmin(t.a.z, t.b.z), t.c.z)),
+                    v3(std::fmax(std::fmax(t.a.x, t.b.x), t.c.x), std::fmax(std::fmax(t.a.y, t.b.y), t.c.y),
+                       std::fmax(std::fmax(t.a.z, t.b.z), t.c.z))};
+            if (T->qbits) tb = quant(tb, T->qref ? *T->qref : box, T->qbits);
+            if (!near(tb, ray, pad)) {
+                ++c.tri_culled;
+                continue;
+            }
+        }
         ++c.tris;
         if (tri_intersect(m.tri(id), ray, &hh)) {
             if (!any || hh.t < h->t) { *h = hh; *tri = id; any = true; }
@@ -228,11 +241,12 @@ int main(int argc, char** argv) {
         V3 y = L + norm(v3(std::sqrt(1 - zz * zz) * std::cos(ph), std::sqrt(1 - zz * zz) * std::sin(ph), zz)) * 4.0;
         Q.push_back(Ray{h.pos, norm(y - h.pos)});
     }
-    Tight T2 = T, T3 = T, T4 = T;
+    Tight T2 = T, T3 = T, T4 = T, T5 = T;
+    T5.after = true; T5.qbits = 16; T5.qref = &M.bbox; T5.tri_cull = true;
     T2.after = true;
     T3.after = true; T3.qbits = 8;
     T4.after = true; T4.qbits = 16; T4.qref = &M.bbox;
-    Counts base, tight, after, q8, q16;
+    Counts base, tight, after, q8, q16, q16t;
     long past = 0, root_dead = 0, miss_walks = 0;
     for (const Ray& r : Q) {
         if (!near(M.bbox, r, pad) && !near(M.oct_bbox, r, pad)) continue;
@@ -245,6 +259,14 @@ int main(int argc, char** argv) {
         walk(M, 0, M.oct_bbox, r, &h3, &t3, after, &T2, pad, rocts);
         walk(M, 0, M.oct_bbox, r, &h3, &t3, q8, &T3, pad, rocts);
         walk(M, 0, M.oct_bbox, r, &h3, &t3, q16, &T4, pad, rocts);
+        {
+            Hit h5; int t5 = -1;
+            const bool e = walk(M, 0, M.oct_bbox, r, &h5, &t5, q16t, &T5, pad, rocts);
+            if (e != a || (a && (t5 != t1 || std::memcmp(&h1.t, &h5.t, 8) != 0))) {
+                std::fprintf(stderr, "MISMATCH: triangle-bounds culling changed a result\n");
+                return 2;
+            }
+        }
         {  // would a pre-test of the root children's subtree bounds have rejected this walk?
             bool any = false;
             for (int k = 0; k < 8; ++k) {
@@ -275,6 +297,9 @@ int main(int argc, char** argv) {
     pr("after", after);
     pr("q8", q8);
     pr("q16 mesh", q16);
+    pr("q16+tri", q16t);
+    std::printf("q16+tri: triangle tests culled by the triangle's own bounds %.2f per walk (of %.2f)\n",
+                (double)q16t.tri_culled / past, (double)(q16t.tri_culled + q16t.tris) / past);
     std::printf("f32 octant classification (margin 1e-5 of the box extent): %ld tests, %.4f ambiguous\n", base.f32_tests,
                 (double)base.f32_amb / std::max(1L, base.f32_tests));
     return 0;
