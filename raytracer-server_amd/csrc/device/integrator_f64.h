@@ -151,7 +151,7 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
     RT_DBG_TEND(7, t_sf);
     if (ps.kind == K_CAMERA) {
         ps.L = ld3(obj.emitted);
-    } else if (ps.kind == K_SPEC) {
+    } else if (!C::nospec && ps.kind == K_SPEC) {
         ps.L = ps.L + mult(cold.bemit(ps), ld3(obj.emitted));
     } else if (C::mis && hr.obj == sc.light && ps.pdf_prev > 0.0) {
         // MIS, BSDF strategy: emitted radiance with the balance-heuristic weight
@@ -161,11 +161,11 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
         ps.L = ps.L + mult(ps.beta, ld3(obj.emitted) * wgt);
     }
     V3 o = -ps.ray.d;  // the out direction, except after a mirror bounce (which keeps the previous one)
-    if (ps.kind == K_SPEC) o = cold.o(ps);
+    if (!C::nospec && ps.kind == K_SPEC) o = cold.o(ps);
     ps.depth += 1;
     const double p = ps.depth <= (uint32_t)MAX_BOUNCES ? 1.0 : SURVIVAL_PROBABILITY;
     Rng rng(ps.r0, ps.r1);
-    const bool spec = obj.brdf == BRDF_SPECULAR;
+    const bool spec = !C::nospec && obj.brdf == BRDF_SPECULAR;
 #if !RT_OPT_SPEC
     if (spec) {
         RT_DBG_REGION(7);

@@ -1186,6 +1186,7 @@ struct Cfg {
     static constexpr bool mis = (F & 4) != 0;    // RT_FLAG_MIS
     static constexpr bool compact = (F & 8) != 0;  // scene fits the compact tables (DevScene)
     static constexpr bool bvh = (F & 16) != 0;     // RT_FLAG_MESH_NEAREST: nearest-triangle meshes via the BVH
+    static constexpr bool nospec = (F & 32) != 0;  // no specular (mirror) object: the mirror paths compile out
 };
 
 // Per-call view of the compact tables (scene_layout.h: CompactTab). The empty asm makes the pointer
@@ -1534,7 +1535,8 @@ RT_DEV V3 brdf_eval(const DevObject& o, V3 n, V3 out, V3 in) {
 #ifndef RT_OPT_KPI
 #define RT_OPT_KPI 1  // A/B: diffuse f = kd * FRAC_1_PI read from the object (host-evaluated, same bits)
 #endif
-    if (o.brdf == BRDF_DIFFUSE) return RT_OPT_KPI ? ld3(o.kpi) : ld3(o.k) * FRAC_1_PI;
+    // (every object of a scene without Phong or mirror objects is diffuse)
+    if ((C::nospec && !C::phong) || o.brdf == BRDF_DIFFUSE) return RT_OPT_KPI ? ld3(o.kpi) : ld3(o.k) * FRAC_1_PI;
     if (!C::phong || o.brdf == BRDF_SPECULAR) {
         if (equal_within(in, flip_across(out, n), 0.001)) return ld3(o.k) / dot(n, in);
         return v3(0, 0, 0);
@@ -1553,7 +1555,7 @@ RT_DEV void local_coord(V3 n, V3* u, V3* v, V3* w) {
 // sample_incoming (scene.rs:56-98); draws: u1 = d[3], u2 = d[4], u3 = d[5].
 template <class C>
 RT_DEV void brdf_sample(const DevObject& o, V3 n, V3 out, Rng& rng, V3* in, double* pdf) {
-    if (o.brdf == BRDF_DIFFUSE) {
+    if ((C::nospec && !C::phong) || o.brdf == BRDF_DIFFUSE) {
         double z = sqrt_rn(rng.uniform());
         double r = sqrt_rn(1.0 - z * z);
         double phi = 2.0 * PI * rng.uniform();

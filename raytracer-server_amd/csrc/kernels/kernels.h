@@ -12,7 +12,8 @@ struct RenderArgs {
     int32_t width, height, x0, y0, tw, th;
     int32_t n_samples;  // spp / 4 per subpixel
     int32_t mis;
-    int32_t features;  // Cfg<F> bits: 1 mesh, 2 phong, 4 mis, 8 compact, 16 nearest-triangle meshes (BVH)
+    int32_t features;  // Cfg<F> bits: 1 mesh, 2 phong, 4 mis, 8 compact, 16 nearest-triangle meshes (BVH),
+                       // 32 no mirror (specular) object (the query-pool kernel's Cfg; the others ignore it)
     int32_t mesh_nodes;  // octree nodes of the largest mesh (megakernel choice)
     int32_t row_step;    // tile row i = screen row y0 + i * row_step
     int32_t tail_cps;    // split tail: chunks per subpixel

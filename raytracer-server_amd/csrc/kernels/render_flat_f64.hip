@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "../device/integrator_f64.h"
 #include "kernels.h"
@@ -507,7 +508,7 @@ constexpr int kFpRing = 512;  // per mesh: at most 256 closest-hit + 256 shadow 
 
 template <int F, int W>
 __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
-                                                                 uint32_t* next_sub, long nsub, int pool_min) {
+                                                                 uint32_t* next_sub, long nsub, int pool_min, int refill) {
     using C = Cfg<F>;
     static_assert(C::mesh && C::compact && !C::bvh, "flat-mesh kernel: compact scenes, octree meshes");
     DevScene sc = sc_g;
@@ -533,8 +534,18 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
     __shared__ double s_rt[kFlatMeshes * kBlk];
     __shared__ uint8_t s_rp[kFlatMeshes * kBlk];
     __shared__ uint8_t s_ro[kFlatMeshes * kBlk];
-    __shared__ double s_cold[6 * kBlk];
-    const LdsCold cold{(LdsD*)s_cold + threadIdx.x};
+    // Scenes without a mirror object (Cfg::nospec) have no mirror-bounce state: its 12 KB hold a
+    // camera-sample buffer instead (as k_megakernel_f64's: the next sample's camera ray and RNG state,
+    // computed for many lanes at once in a refill pass rather than by a few lanes per iteration).
+    __shared__ double s_cold[C::nospec ? 1 : 6 * kBlk];
+    using Cold = std::conditional_t<C::nospec, RegCold, LdsCold>;
+    Cold cold{};
+    if constexpr (!C::nospec) cold = LdsCold{(LdsD*)s_cold + threadIdx.x};
+    __shared__ double s_nbd[C::nospec ? 3 * kBlk : 1];
+    __shared__ uint64_t s_nbr[C::nospec ? 2 * kBlk : 1];
+    LdsD* nbd = (LdsD*)s_nbd + (C::nospec ? threadIdx.x : 0);
+    __attribute__((address_space(3))) uint64_t* nbr = (__attribute__((address_space(3))) uint64_t*)s_nbr + (C::nospec ? threadIdx.x : 0);
+    bool nvalid = false;  // nbd / nbr hold sample s + 1 of subpixel id
     __shared__ int32_t s_pend[kBlk];
     // per mesh: queued queries, entry = lane (closest hit) or 256 + lane (shadow)
     __shared__ int32_t s_ring[kFlatMeshes][kFpRing];
@@ -638,7 +649,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                 nverts += h.obj >= 0;
                 ShadowDefer df;
                 df.pending = false;
-                const bool cont = shade_vertex<C, LdsCold>(sc, a, ps, h, &df, cold);
+                const bool cont = shade_vertex<C, Cold>(sc, a, ps, h, &df, cold);
                 traced = false;
                 if (df.pending) {  // the analytic objects let the shadow ray through; a mesh may block it
                     shadow_q = true;
@@ -689,6 +700,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                     if (++id < end) {  // the next subpixel of the run, no ticket
                         s = 0;
                         acc_l[0] = 0.0; acc_l[kBlk] = 0.0; acc_l[2 * kBlk] = 0.0;
+                        nvalid = false;
                     } else {
                         done = true;
                     }
@@ -711,13 +723,29 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
             active = !stop && nt < nunits;
             acc_l[0] = 0.0; acc_l[kBlk] = 0.0; acc_l[2 * kBlk] = 0.0;
             fresh = true;
+            nvalid = false;
+        }
+        // camera-sample refill pass (no-mirror scenes): lanes with a sample in progress and a next
+        // sample in the same unit, once at least `refill` of the wave's lanes need one
+        if constexpr (C::nospec) {
+            const bool need = active && !fresh && !nvalid && unit_has_next(a, id, s);
+            if (refill > 0 && __popcll(__ballot(need)) >= refill) {
+                if (need) {
+                    const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), s + 1);
+                    nbd[0] = nb.d.x; nbd[kBlk] = nb.d.y; nbd[2 * kBlk] = nb.d.z;
+                    nbr[0] = nb.r0; nbr[kBlk] = nb.r1;
+                    nvalid = true;
+                }
+            }
         }
         // ---------------- the next ray (the path goes on, or a new sample), its closest-hit queries
         const bool tr = ready && active && !endwait && !traced;
         uint32_t want_c = 0;
         if (tr) {
             if (fresh) {
-                begin_sample(sc, a, subpixel_of(a, id), s, ps);
+                if (C::nospec && nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[kBlk], nbd[2 * kBlk]), nbr[0], nbr[kBlk]}, ps);
+                else begin_sample(sc, a, subpixel_of(a, id), s, ps);
+                nvalid = false;
                 fresh = false;
             }
             const RayInv inv = make_inv(ps.ray.d);
@@ -755,11 +783,11 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
 
 template <int F, int W>
 static void launch_fpool(const DevScene& sc, RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
-                         double* tail_buf, size_t tail_cap, int pool_min, hipStream_t st) {
+                         double* tail_buf, size_t tail_cap, int pool_min, int refill, hipStream_t st) {
     const long blocks = resident_blocks(k_megakernel_fpool_f64<F, W>, (nsub + kBlk - 1) / kBlk);
     plan_tail(a, nsub, blocks * kBlk, tail_buf, tail_cap);
     hipLaunchKernelGGL((k_megakernel_fpool_f64<F, W>), dim3((unsigned)blocks), dim3(kBlk), 0, st, sc, a, sub_buf,
-                       next_sub, nsub, pool_min);
+                       next_sub, nsub, pool_min, refill);
 }
 
 template <int F, int W>
@@ -780,17 +808,31 @@ hipError_t launch_megakernel_flat_f64(const DevScene& sc, const RenderArgs& a_in
     static const int waves = env_int("RT_MK_FLAT_WAVES", 3);
     static const int fpool = env_int("RT_MK_FPOOL", 1);
     static const int pool_min = env_int("RT_MK_FPOOL_MIN", 48);
+    static const int nospec = env_int("RT_MK_NOSPEC", 1);  // A/B: 0 = the mirror-capable kernel for every scene
+    // camera-sample refill threshold of the query-pool kernel (no-mirror scenes): 16-24 lanes measured
+    // best on the cubes (8: 736.9, 16: 747.2, 24: 745.2, 32: 737.3, 40: 730.9 Msamples/s; the analytic
+    // kernel's `refill` is 40)
+    static const int fpool_refill = env_int("RT_MK_FPOOL_REFILL", 20);
+    (void)refill;
 #define RT_FLAT_CASE(F)                                                                       \
     case F:                                                                                   \
         if (fpool) {                                                                          \
-            if (waves == 2) launch_fpool<F, 2>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, st); \
-            else launch_fpool<F, 3>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, st); \
+            if (waves == 2) launch_fpool<F, 2>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); \
+            else launch_fpool<F, 3>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); \
         } else if (waves == 2) launch_flat<F, 2>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, st); \
         else launch_flat<F, 3>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, st); \
         break;
-    switch (a.features & 15) {
-        RT_FLAT_CASE(9) RT_FLAT_CASE(11) RT_FLAT_CASE(13) RT_FLAT_CASE(15)
-        default: return hipErrorInvalidValue;
+    if (fpool && nospec && (a.features & 32) && !(a.features & 2)) {  // no mirror, no Phong object
+        switch (a.features & 15) {
+            case 9: launch_fpool<9 | 32, 3>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); break;
+            case 13: launch_fpool<13 | 32, 3>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); break;
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (a.features & 15) {
+            RT_FLAT_CASE(9) RT_FLAT_CASE(11) RT_FLAT_CASE(13) RT_FLAT_CASE(15)
+            default: return hipErrorInvalidValue;
+        }
     }
 #undef RT_FLAT_CASE
     launch_tail_sum_f64(a, sub_buf, nsub - a.n_whole, st);

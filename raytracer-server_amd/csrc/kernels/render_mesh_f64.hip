@@ -292,6 +292,9 @@ enum : uint8_t { POOL_CLOSEST = 0, POOL_SHADOW = 1, POOL_DONE = 2 };
 #ifndef RT_POOL_REFILL
 #define RT_POOL_REFILL 32
 #endif
+#ifndef RT_POOL_CAMBUF
+#define RT_POOL_CAMBUF 1  // A/B: the walk pool keeps a camera-sample buffer (refill pass) as k_megakernel_f64
+#endif
 constexpr int kPoolRefill = RT_POOL_REFILL;  // refill only when at least this many lanes of the round are idle
 
 // Compact park of the walk pool (fits 3 blocks of 256 threads per CU, i.e. 3 waves/SIMD): no 1/d
@@ -300,7 +303,8 @@ constexpr int kPoolRefill = RT_POOL_REFILL;  // refill only when at least this m
 // query t (closest hit so far / shadow distance). Ints: cur, depth | pm << 8 | stk8 << 16, path,
 // stk (2 words), order, lpos, lend, best, hit object, hit prim, gen slot, mesh, occluded.
 #ifndef RT_PARK_INV
-#define RT_PARK_INV 1  // A/B: the park keeps 1/d (1) or park2_load recomputes it (0)
+#define RT_PARK_INV 0  // A/B: the park keeps 1/d (1) or park2_load recomputes it (0; its 6 KB of LDS hold the
+                       // pool's camera-sample buffer instead, RT_POOL_CAMBUF)
 #endif
 constexpr int kPark2D = RT_PARK_INV ? 17 : 14, kPark2I = RT_WALK_READAHEAD ? 18 : 17;
 enum : int { P2_T = 13, P2_HOBJ = 9, P2_HPRIM = 10, P2_OCC = 13, P2_NEAR = 16 };
@@ -500,14 +504,15 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
         }
         __syncthreads();
     }
-    // subpixel accumulator and camera-sample buffer in LDS, as in k_megakernel_f64
-    // (no camera-sample buffer in pool mode: its 10 KB of LDS are what a third block per CU needs)
-    __shared__ double s_acc[3 * 256], s_nbd[P ? 1 : 3 * 256];
-    __shared__ uint64_t s_nbr[P ? 1 : 2 * 256];
+    // subpixel accumulator and camera-sample buffer in LDS, as in k_megakernel_f64 (pool mode: the
+    // buffer's 10 KB fit beside the park at 2 blocks per CU without the parked 1/d, RT_PARK_INV = 0)
+    constexpr bool kCamBuf = !P || RT_POOL_CAMBUF;
+    __shared__ double s_acc[3 * 256], s_nbd[kCamBuf ? 3 * 256 : 1];
+    __shared__ uint64_t s_nbr[kCamBuf ? 2 * 256 : 1];
     LdsDouble* acc_l = (LdsDouble*)s_acc + threadIdx.x;
-    LdsDouble* nbd = (LdsDouble*)s_nbd + (P ? 0 : threadIdx.x);
-    LdsU64* nbr = (LdsU64*)s_nbr + (P ? 0 : threadIdx.x);
-    if constexpr (P) refill = 0;
+    LdsDouble* nbd = (LdsDouble*)s_nbd + (kCamBuf ? threadIdx.x : 0);
+    LdsU64* nbr = (LdsU64*)s_nbr + (kCamBuf ? threadIdx.x : 0);
+    if constexpr (!kCamBuf) refill = 0;
     V3 pc = v3(0, 0, 0);  // pool: the pending shadow query's NEE term (the park has no room for it)
     uint32_t nverts = 0;
     // tickets: whole subpixels, then the split tail's chunks (unit_of), as in k_megakernel_f64
@@ -615,7 +620,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
             // the next ray, unless a shadow query is pending or the unit is done (a new ticket first)
             if (!walking && !done) {
                 if (fresh) {
-                    begin_sample(sc, a, subpixel_of(a, id), s, ps);
+                    if (kCamBuf && nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[256], nbd[512]), nbr[0], nbr[256]}, ps);
+                    else begin_sample(sc, a, subpixel_of(a, id), s, ps);
+                    nvalid = false;
                     fresh = false;
                 }
                 RT_DBG_TSTART(t_ta);
@@ -783,10 +790,11 @@ hipError_t launch_megakernel_mesh_f64(const DevScene& sc, const RenderArgs& a, d
     static const int pool_min = env_int("RT_MK_POOL_MIN", 32);
     static const int pool_ksteps = std::max(1, env_int("RT_MK_POOL_KSTEPS", 6));
     static const int pool_vmin = env_int("RT_MK_POOL_VMIN", 0);
+    static const int pool_refill = env_int("RT_MK_POOL_CAM_REFILL", 20);  // the walk pool's camera refill threshold
 #define RT_MM_CASE(F)                                                                          \
     case F:                                                                                    \
-        if (pool == 3) launch_mm<F, 3, 1>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
-        else if (pool) launch_mm<F, 2, 1>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
+        if (pool == 3) launch_mm<F, 3, 1>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, pool_refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
+        else if (pool) launch_mm<F, 2, 1>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, pool_refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
         else launch_mm<F, 2, 0>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, 0, 0, tail_buf, tail_cap, st); \
         break;
 #define RT_MMB_CASE(F)                                                                         \

@@ -937,9 +937,13 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
     a.n_samples = p->spp > 0 ? p->spp / 4 : 0;  // server.rs:332 (i32 division)
     a.mis = (p->flags & RT_FLAG_MIS) ? 1 : 0;
     {
-        bool phong = false;
-        for (const auto& o : s->host.objects) phong |= o.brdf == RT_BRDF_PHONG;
-        a.features = (s->host.meshes.empty() ? 0 : 1) | (phong ? 2 : 0) | (a.mis ? 4 : 0) | (ds.compact ? 8 : 0);
+        bool phong = false, spec = false;
+        for (const auto& o : s->host.objects) {
+            phong |= o.brdf == RT_BRDF_PHONG;
+            spec |= o.brdf == RT_BRDF_SPECULAR;
+        }
+        a.features = (s->host.meshes.empty() ? 0 : 1) | (phong ? 2 : 0) | (a.mis ? 4 : 0) | (ds.compact ? 8 : 0) |
+                     (spec ? 0 : 32);
         if ((p->flags & RT_FLAG_MESH_NEAREST) && !s->host.meshes.empty()) a.features |= 16;
         for (const auto& m : s->host.meshes) a.mesh_nodes = std::max(a.mesh_nodes, (int32_t)m.octree.size());
         a.all_flat = !s->packed.meshes.empty() && s->packed.meshes.size() <= (size_t)rt::kFlatMeshes;
