@@ -108,13 +108,16 @@ print(json.dumps(out))
 """
 
 
-@pytest.mark.parametrize("env", [{"RT_MK_FPOOL": "0"}, {"RT_MK_POOL": "0"}, {"RT_MK_POOL": "3"}])
+@pytest.mark.parametrize("env", [{"RT_MK_FPOOL": "0"}, {"RT_MK_POOL": "0"}, {"RT_MK_POOL": "3"}, {"RT_MK_NOSPEC": "0"},
+                                 {"RT_MK_FPOOL_REFILL": "0", "RT_MK_POOL_CAM_REFILL": "0"}])
 def test_kernel_variants_render_the_default_frames(env):
     """The A/B kernel variants behind RT_* switches (read once per process, so each in a subprocess):
-    the block-synchronous flat kernel (RT_MK_FPOOL=0), per-lane octree walks (RT_MK_POOL=0) and the
-    walk pool at 3 waves/SIMD (RT_MK_POOL=3) render byte-identical frames to the defaults."""
+    the block-synchronous flat kernel (RT_MK_FPOOL=0), per-lane octree walks (RT_MK_POOL=0), the
+    walk pool at 3 waves/SIMD (RT_MK_POOL=3), the mirror-capable query-pool instance on the mirror-free
+    cubes (RT_MK_NOSPEC=0: the default runs Cfg bit 32) and both pools without their camera-sample
+    refill pass render byte-identical frames to the defaults."""
     base = dict(os.environ, RT_REPO=REPO)
-    for k in ("RT_MK_FPOOL", "RT_MK_POOL"):
+    for k in ("RT_MK_FPOOL", "RT_MK_POOL", "RT_MK_NOSPEC", "RT_MK_FPOOL_REFILL", "RT_MK_POOL_CAM_REFILL"):
         base.pop(k, None)
     runs = []
     for e in ({}, env):
