@@ -504,9 +504,6 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
 // that ray's closest-hit queries. A path thus waits only for its own queries, queries are evaluated
 // in fuller chunks, and no wave waits at a barrier for another wave's chunk (the block-synchronous
 // kernel spent 24% of its wave time in barrier waits, 2 waves of 4 working in phase P).
-#ifndef RT_FPOOL_LDSPC
-#define RT_FPOOL_LDSPC 0  // A/B: the query pool's pending NEE term in LDS instead of VGPRs (no LDS object table)
-#endif
 constexpr int kFpRing = 512;  // per mesh: at most 256 closest-hit + 256 shadow queries queued at once
 
 template <int F, int W>
@@ -515,7 +512,6 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
     using C = Cfg<F>;
     static_assert(C::mesh && C::compact && !C::bvh, "flat-mesh kernel: compact scenes, octree meshes");
     DevScene sc = sc_g;
-#if !RT_FPOOL_LDSPC
     __shared__ DevObject s_objs[kMaxCompactObjects];
     {
         const uint64_t* src = reinterpret_cast<const uint64_t*>(sc_g.objects);
@@ -524,7 +520,6 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
         for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
         sc.objects = s_objs;
     }
-#endif
     // per lane (one column per thread): subpixel accumulator; the closest-hit query ray (o, d), the
     // shadow query ray (o, d, |y - x|); results per (mesh, lane); queries outstanding per lane
     // The closest-hit and the shadow query of a lane are issued in the same iteration from the same
@@ -582,17 +577,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
     bool endwait = false;  // the path has ended; the sample is finished once the shadow result is in
     HitRec h{0.0, -1, -1};
     uint32_t qmask = 0, smask = 0;
-#if RT_FPOOL_LDSPC
-    // the pending NEE term in an LDS column (6 VGPRs less; the object table stays in global memory)
-    __shared__ double s_pc[3 * kBlk];
-    LdsD* pcl = (LdsD*)s_pc + tid;
-#define RT_PC_GET() v3(pcl[0], pcl[kBlk], pcl[2 * kBlk])
-#define RT_PC_SET(v) do { const V3 v_ = (v); pcl[0] = v_.x; pcl[kBlk] = v_.y; pcl[2 * kBlk] = v_.z; } while (0)
-#else
     V3 pc = v3(0, 0, 0);
-#define RT_PC_GET() pc
-#define RT_PC_SET(v) (pc = (v))
-#endif
     while (__any(active)) {
         RT_DBG_WAVE(8, lane_id_is0());
         RT_DBG_TSTART(t_q);
@@ -645,7 +630,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                 bool occluded = false;
                 for (int m = 0; m < nm; ++m)
                     if ((smask >> m) & 1u) occluded |= s_ro[m * kBlk + tid] != 0;
-                if (!occluded) ps.L = ps.L + RT_PC_GET();
+                if (!occluded) ps.L = ps.L + pc;
                 spend = false;
             }
             if (endwait) {
@@ -668,7 +653,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                 traced = false;
                 if (df.pending) {  // the analytic objects let the shadow ray through; a mesh may block it
                     shadow_q = true;
-                    RT_PC_SET(df.c);
+                    pc = df.c;
                     dist = df.dist;
                     sr = Ray{df.o, df.d};
                     near_s = df.meshes;
@@ -692,7 +677,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                 spend = true;
                 smask = want_s;
             } else {  // no mesh near the shadow segment: unblocked now
-                ps.L = ps.L + RT_PC_GET();
+                ps.L = ps.L + pc;
                 if (endwait) {
                     endwait = false;
                     finish = true;
