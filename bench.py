@@ -11,11 +11,14 @@ fixed: scaling = "strong". Rank 0 prints one JSON line.
 
 roofline (dominant kernel = the render megakernel; kernel_ms = its average device time per launch,
 HIP events recorded on the stream the kernel runs on):
-  * bound "hbm" with SURVEY §8(d)'s algorithmic bytes, the figure §8(d) names for roofline.achieved:
+  * bound "valu_issue_f64" (what limits the megakernel, detailed in `compute` below); achieved / peak /
+    frac keep SURVEY §8(d)'s algorithmic bytes, the figure §8(d) names for roofline.achieved:
     88 B per camera sample + 280 B per path vertex (the canonical f32 SoA wavefront's state traffic;
     vertices = this run's device counter) over kernel_ms; peak 8.0 TB/s; frac = achieved / peak.
     The megakernel does not stream that state (a path lives in registers), so this is the rate the
-    kernel's throughput corresponds to on §8(d)'s roofline, not bytes it moves;
+    kernel's throughput corresponds to on §8(d)'s roofline, not bytes it moves. model_ceiling_Msamples
+    = 8 TB/s / (88 + 280 V) with V = vertices per sample: the rate at which that model reaches the HBM
+    peak (a faster kernel reads as beating the wavefront model, frac > 1, not as moving > 8 TB/s);
   * traffic = the HBM bytes the PMC counters measured for one launch of this exact command
     (profiles/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE, separate rocprofv3 passes over
     `bench.py --steps 1 --warmup 0`, tools/gpu_task.sh benchpmc), scaled to this rank's rows; null
@@ -207,11 +210,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # device map: rank -> its local GPU; RT_BENCH_DEVICE=k puts every rank on GPU k (a rehearsal of the
+    # N-rank path on a one-GPU box: the frame digest must equal N = 1's, the timing means nothing)
+    pinned = os.environ.get("RT_BENCH_DEVICE")
+    device = int(pinned) if pinned not in (None, "") else (local if world > 1 else 0)
+    torch.cuda.set_device(device)
     if world > 1:
-        torch.cuda.set_device(local)
         dist.init_process_group("gloo")  # host gather + barriers; no RCCL on the data path
-    else:
-        torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
 
     import rt_amd
@@ -315,12 +320,20 @@ def main():
                        "parallelism": f"{'interleaved rows' if args.partition == 'interleave' else 'row stripes'} x{world}"
                                       ", host gather (gloo)" if world > 1 else "1 GPU",
                        "frame_sha1": digest,
+                       "device_map": f"every rank on GPU {device} (RT_BENCH_DEVICE: a rehearsal, timing not "
+                                     "meaningful)" if pinned not in (None, "") else "rank -> LOCAL_RANK",
                        "vertices": total_vertices,
                        "vertices_per_sample": round(total_vertices / n_samples, 4)},
-            "roofline": {"bound": "hbm",
+            "roofline": {"bound": "valu_issue_f64" if args.mode == "megakernel" else "hbm",
                          "achieved": round(model_gbs, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(model_gbs / HBM_PEAK_GBS, 4),
+                         "frac_meaning": "SURVEY 8(d)'s wavefront model: the f32 SoA state bytes this throughput "
+                                         "would stream, over 8 TB/s (a model ceiling, not bytes moved; the "
+                                         "megakernel keeps its paths in registers and is bound by f64 VALU issue, "
+                                         "roofline.compute)",
+                         "model_ceiling_Msamples": round(HBM_PEAK_GBS * 1e9 / (BYTES_PER_SAMPLE + BYTES_PER_VERTEX
+                                                         * st["vertices"] / rank_samples) / 1e6, 1),
                          "traffic": traffic,
                          "algorithmic_bytes_per_launch": model_bytes,
                          "algorithmic_model": "SURVEY 8(d): 88 B per camera sample + 280 B per path vertex (f32 SoA "

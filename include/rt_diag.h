@@ -8,10 +8,12 @@
 extern "C" {
 #endif
 /* Device self-test of the exact-arithmetic shortcuts (path_f64.h: rcp_rn, qdiv, sqrt_rn) against
- * the IEEE operations on n pseudo-random operands on the current HIP device; out[0] = reciprocal
- * mismatches, out[1] = quotient mismatches, out[2] = square-root mismatches (sqrt_rn's fast range
- * [2^-767, 2^1024) against the library sqrt). Returns 0 or -1 (HIP error). */
-int rt_selftest_arith(long n, unsigned long long seed, unsigned long long out[3]);
+ * the IEEE operations on n pseudo-random operands on the current HIP device; writes min(n_out, 3)
+ * counts: out[0] = reciprocal mismatches, out[1] = quotient mismatches, out[2] = square-root
+ * mismatches (sqrt_rn's fast range [2^-767, 2^1024) against the library sqrt). Returns 0 or -1. */
+int rt_selftest_arith_n(long n, unsigned long long seed, unsigned long long* out, int n_out);
+/* The original entry point: out[0] reciprocal and out[1] quotient mismatches only. */
+int rt_selftest_arith(long n, unsigned long long seed, unsigned long long out[2]);
 /* RT_QCHECK builds (-DRT_QCHECK=1): counters of LDS hand-off protocol violations in the megakernels'
  * work queues since the last call (kernels/megakernel_common.h): [0] ring slot overwritten / bad
  * entry, [1] queue over capacity, [2] outstanding-query count below zero, [3] owner/taker state

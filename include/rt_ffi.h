@@ -124,7 +124,9 @@ void rt_scene_destroy(rt_scene* scene);
 
 /* Scene inspection (host prep parity: octree shape etc.). info[16] int64:
  * [0]=objects [1]=light index [2]=meshes [3]=total octree nodes [4]=parents [5]=leaves
- * [6]=triangle refs [7]=triangles [8]=vertices [9]=max leaf size [10]=max leaf depth */
+ * [6]=triangle refs [7]=triangles [8]=vertices [9]=max leaf size [10]=max leaf depth
+ * [11]=1 if the octree walks use the child-slot tables (subtree culls), 0 if they read the plain child
+ * tables (octrees whose node ids exceed the slot encoding, 2^23; same results either way) */
 int rt_scene_info(const rt_scene* scene, int64_t info[16]);
 /* Per-object mesh data after transforms: bbox[6], surface area, octree in DFS pre-order
  * (kind: 0 parent/1 leaf, child[8*n], leaf_off, leaf_cnt, refs). Any output pointer may be NULL. */

@@ -579,49 +579,17 @@ struct OctWalk {
     uint32_t ndone;
     uint32_t enter;  // slot walk: the root is still to be entered (its octant_mask runs in the first step,
                      // in the same code as every descent's)
-    // Read-ahead of the next descent (the walk's dependent load chain: pick a child entry -> load that
-    // node's 8 child entries -> octant_mask -> pick ...): walk_enter takes the entry of the first child
-    // in visiting order from the node's child table it has in registers (nc), and when that child is
-    // a parent node below the LDS top levels, issues the load of ITS 8 child entries right away (pka,
-    // pkb), so the next step's pick needs no load and its walk_enter finds the entries arrived.
-    int32_t nc;           // the next pick's child entry at `cur`, or kNcNone (read it from the table)
-    int4 pka, pkb;        // node nc's child entries, loaded ahead (nc a parent below the top levels)
 };
-constexpr int32_t kNcNone = (int32_t)0x80000000;
 
-// Mask `cur`'s existing children whose boxes the ray hits, permuted to visiting order. (The child
-// table itself is not kept in registers: a pick reads its one entry again, an L2 hit.)
-// `top`: the LDS copy of this mesh's top levels (scene_layout.h: top_slot), or null; a node at depth
-// <= kTopDepth is then read from it (ds_read) instead of node_kids.
-typedef __attribute__((address_space(3))) int32_t LdsTopI32;
-#ifndef RT_WALK_READAHEAD
-#define RT_WALK_READAHEAD 0  // A/B: OctWalk::nc / pka / pkb read-ahead of the next descent (1: measured 5% slower
-                             // on the unicorn, 141.4 vs 148.4 Msamples/s, profiles/r03_ab.log) or none (0)
-#endif
-// Loads node `node`'s child entries (from the LDS top levels when it sits there).
-RT_DEV void node_kids4(const DevScene& sc, int32_t node, int depth, uint32_t path, const LdsTopI32* top, int4& ka,
-                       int4& kb) {
-    if (top && depth <= kTopDepth) {
-        const LdsTopI32* t = top + 8 * top_slot(depth, path);
-        ka = int4{t[0], t[1], t[2], t[3]};
-        kb = int4{t[4], t[5], t[6], t[7]};
-    } else {
-        const int4* k4 = reinterpret_cast<const int4*>(sc.node_kids + 8 * (size_t)node);
-        ka = k4[0];
-        kb = k4[1];
-    }
-}
-// `pre`: cur's child entries loaded ahead (OctWalk::pka / pkb), or null to load them here.
-RT_DEV void walk_enter(const DevScene& sc, const Ray& ray, const RayInv& inv, OctWalk& w,
-                       const LdsTopI32* top = nullptr, bool pre = false) {
+// LDS column of a walk's ancestor node ids (walk_node_slots' `anc`)
+typedef __attribute__((address_space(3))) int32_t LdsAncI32;
+
+// Mask `cur`'s existing children whose boxes the ray hits, permuted to visiting order (the node_kids
+// walk: the child table is read again by each pick, an L2 hit).
+RT_DEV void walk_enter(const DevScene& sc, const Ray& ray, const RayInv& inv, OctWalk& w) {
     RT_DBG(2);
-    int4 ka, kb;
-    if (pre) {
-        ka = w.pka;
-        kb = w.pkb;
-    } else {
-        node_kids4(sc, w.cur, w.depth, w.path, top, ka, kb);
-    }
+    const int4* k4 = reinterpret_cast<const int4*>(sc.node_kids + 8 * (size_t)w.cur);
+    const int4 ka = k4[0], kb = k4[1];
     const int32_t kid[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
     uint32_t m = octant_mask(w.mn, w.mx, ray, inv);
 #pragma unroll
@@ -630,21 +598,6 @@ RT_DEV void walk_enter(const DevScene& sc, const Ray& ray, const RayInv& inv, Oc
 #pragma unroll
     for (int q = 0; q < 8; ++q) pm |= ((m >> ((w.order >> (4 * q)) & 0xF)) & 1u) << q;
     w.pm = pm;
-    w.nc = kNcNone;
-#if RT_WALK_READAHEAD
-    if (pm) {  // the first child in visiting order: the next pick's entry, and its own children ahead
-        const uint32_t oi = (w.order >> (4 * __builtin_ctz(pm))) & 0xF;
-        int32_t c = kid[0];
-#pragma unroll
-        for (int i = 1; i < 8; ++i) c = oi == (uint32_t)i ? kid[i] : c;
-        w.nc = c;
-        if (c >= 0 && !(top && w.depth + 1 <= kTopDepth)) {
-            const int4* k4 = reinterpret_cast<const int4*>(sc.node_kids + 8 * (size_t)c);
-            w.pka = k4[0];
-            w.pkb = k4[1];
-        }
-    }
-#endif
 }
 // walk_enter for the slot walk: the node's existence mask comes with its parent's slot entry
 // (scene_layout.h KidSlot), so entering a node loads nothing.
@@ -654,30 +607,18 @@ RT_DEV void walk_enter_mask(const Ray& ray, const RayInv& inv, OctWalk& w, uint3
     uint32_t pm = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) pm |= ((m >> ((w.order >> (4 * q)) & 0xF)) & 1u) << q;
-    w.pm = pm;  // (w.nc is not used by the slot walk; a store to it here let the compiler merge it with
-                // another field's store through a computed address, which kept the walk state in scratch)
-}
-// After a walk's state was reloaded (a parked walk): the read-ahead of node nc's entries again.
-RT_DEV void walk_reload_ahead(const DevScene& sc, OctWalk& w, const LdsTopI32* top = nullptr) {
-#if RT_WALK_READAHEAD
-    if (w.nc >= 0 && !(top && w.depth + 1 <= kTopDepth)) {
-        const int4* k4 = reinterpret_cast<const int4*>(sc.node_kids + 8 * (size_t)w.nc);
-        w.pka = k4[0];
-        w.pkb = k4[1];
-    }
-#else
-    (void)sc; (void)w; (void)top;
-#endif
+    w.pm = pm;
 }
 
 // Starts a walk; false if the ray cannot produce a usable hit on this mesh (empty mesh, or the
 // conservative near_box cull). tmax: see near_box.
 // Slots: the walk continues with walk_step<true> (the slot walk: the root is entered in its first step),
-// or with walk_step<false> (the node_kids walk: entered here).
-template <bool Slots = (RT_WALK_TIGHT != 0)>
+// or with walk_step<false> (the node_kids walk: entered here). The slot walk needs DevScene::node_slot
+// (absent for octrees whose node ids do not fit a KidSlot entry: rt_api.cpp pack_scene).
 // cull = false: the caller already knows the ray passes near_box for this mesh (mesh_near_mask).
+template <bool Slots = (RT_WALK_TIGHT != 0)>
 RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax,
-                       OctWalk& w, const LdsTopI32* top = nullptr, bool cull = true) {
+                       OctWalk& w, bool cull = true) {
     if (m.n_nodes == 0) return false;
     RT_DBG(0);
     if (cull && !near_box(m.cull_box, ray, inv, m.cull_pad, tmax)) return false;
@@ -693,7 +634,6 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
     w.stk = 0;
     w.stk8 = 0;
     w.pm = 0;
-    w.nc = kNcNone;
     if (m.root_leaf >= 0) {
         const int2 ls = sc.leaf_span[m.root_leaf];
         w.lpos = ls.x;
@@ -722,10 +662,9 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
         w.mx[k] = m.root_box[3 + k];
     }
     if constexpr (Slots) {
-        (void)top;
         w.enter = 1;  // the first step enters the root (walk_node_slots)
     } else {
-        walk_enter(sc, ray, inv, w, top);
+        walk_enter(sc, ray, inv, w);
     }
     return true;
 }
@@ -795,15 +734,6 @@ RT_DEV int leaf_tris(const DevScene& sc, const Ray& ray, OctWalk& w, double* t, 
     }
     return -1;
 }
-// The node part of a walk step (no leaf open, or its triangles exhausted without a hit): pops every
-// exhausted level, then picks the next child in visiting order and either opens it (a leaf: its
-// triangle range in w.lpos / w.lend) or descends into it and masks its children (walk_enter).
-// WALK_RUN, or WALK_MISS once the root is exhausted.
-// `anc` (with `top` only): this walk's LDS column of ancestor node ids at depths kTopDepth + 1 ..
-// kTopDepth + kAncLevels (stride 256 threads), written at each descent from those depths, so a pop
-// reads the ancestor it resumes at from LDS instead of following node_up (one dependent global load
-// per level popped); null: the node_up chain.
-constexpr int kAncLevels = 5;  // depths 4..8: the deepest parents sit at depth 8 (MAX_DEPTH 10, root depth 1)
 // Could any triangle below the child of slot `ks` (scene_layout.h KidSlot) return tri_intersect ==
 // true for this ray? false only if the ray (t >= 0) passes farther than the padding from the child
 // subtree's triangle bounds: the same conservative slab test as near_box. Skipping such a child leaves
@@ -849,7 +779,7 @@ constexpr int kSlotAncLevels = 9;
 #define RT_SLOT_CULL 1  // A/B: 0 = the slot walk without the subtree-bounds test
 #endif  // the deepest parents sit at depth 8 (MAX_DEPTH 10, root depth 1)
 RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w,
-                           LdsTopI32* anc = nullptr) {
+                           LdsAncI32* anc = nullptr) {
     RT_DBG_TSTART(t_pop);
     uint32_t exist = 0;  // a node to enter: its existence mask (the root at a walk's start, or a descent)
     if (w.enter) {
@@ -961,8 +891,13 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
     walk_enter_mask(ray, inv, w, exist);  // one octant_mask for the descents and the walks' starts
     return WALK_RUN;
 }
-RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w,
-                     const LdsTopI32* top = nullptr, LdsTopI32* anc = nullptr) {
+// The node part of a walk step through node_kids (the reference's visiting order without the slot
+// walk's subtree-bounds culls; RT_WALK_TIGHT=0 builds, the wavefront's walk kernels, scenes without
+// slot tables): pops every exhausted level (the ancestor through the node_up links, its box rebuilt
+// from the root), then picks the next child in visiting order and either opens it (a leaf: its
+// triangle range in w.lpos / w.lend) or descends into it and masks its children (walk_enter).
+// WALK_RUN, or WALK_MISS once the root is exhausted.
+RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w) {
     RT_DBG_TSTART(t_pop);
     if (w.pm == 0) {  // `cur` exhausted: resume at the nearest ancestor with children left
         int lv = w.depth;
@@ -975,21 +910,11 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
             RT_DBG_TEND(13, t_pop);
             return WALK_MISS;
         }
-        // the ancestor's node id through the parent links; not needed (and not loaded) when its
-        // level is read from the LDS top levels (w.cur then keeps a stale id >= 0 until the next
-        // descent sets it from a child entry)
-        if (!(top && lv <= kTopDepth)) {
-            if (anc && top && lv <= kTopDepth + kAncLevels) {
-                w.cur = anc[(lv - kTopDepth - 1) * 256];
-            } else {
-                int32_t cur = w.cur;
-                for (int l = w.depth; l > lv; --l) cur = sc.node_up[cur].x;
-                w.cur = cur;
-            }
-        }
+        int32_t cur = w.cur;
+        for (int l = w.depth; l > lv; --l) cur = sc.node_up[cur].x;
+        w.cur = cur;
         w.depth = lv;
         w.pm = pm;
-        w.nc = kNcNone;  // the ancestor's next entry is read from its table
         w.path &= (1u << (3 * lv)) - 1u;
         // the ancestor's box, rebuilt from the root along the path (the build's own arithmetic)
 #pragma unroll
@@ -1011,11 +936,7 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
     const int q = __builtin_ctz(w.pm);
     w.pm &= w.pm - 1u;
     const uint32_t oi = (w.order >> (4 * q)) & 0xF;
-    const bool ahead = RT_WALK_READAHEAD && w.nc != kNcNone;  // the first pick after walk_enter: its entry was read ahead
-    const int32_t c = ahead ? w.nc
-                            : (top && w.depth <= kTopDepth) ? top[8 * top_slot(w.depth, w.path) + (int)oi]
-                                                            : sc.node_kids[8 * (size_t)w.cur + oi];
-    w.nc = kNcNone;
+    const int32_t c = sc.node_kids[8 * (size_t)w.cur + oi];
     if (c <= -2) {  // open a leaf
         RT_DBG(3);
         const int32_t e = -2 - c;  // the leaf's range inline (kid_leaf), or its id behind the escape count
@@ -1033,7 +954,6 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
     }
     // descend: push the remaining mask of `cur`, take the octant's box
     const int lv = w.depth;
-    if (anc && top && lv > kTopDepth && lv <= kTopDepth + kAncLevels) anc[(lv - kTopDepth - 1) * 256] = w.cur;
     if (lv < 8) w.stk = (w.stk & ~(0xFFull << (8 * lv))) | ((uint64_t)w.pm << (8 * lv));
     else w.stk8 = w.pm;
     w.path |= oi << (3 * lv);
@@ -1044,7 +964,7 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         const double cc = (w.mn[k] + w.mx[k]) / 2.0;
         if ((oi >> (2 - k)) & 1u) w.mn[k] = cc; else w.mx[k] = cc;
     }
-    walk_enter(sc, ray, inv, w, top, ahead && !(top && w.depth <= kTopDepth));
+    walk_enter(sc, ray, inv, w);
     RT_DBG_TEND(14, t_pick);
     return WALK_RUN;
 }
@@ -1053,7 +973,7 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
 // walk inlined there trips an AMDGPU backend error, "illegal VGPR to SGPR copy", in ROCm 7.2.)
 template <bool Slots = (RT_WALK_TIGHT != 0)>
 RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w, double* t,
-                     int* prim, const LdsTopI32* top = nullptr, LdsTopI32* anc = nullptr) {
+                     int* prim, LdsAncI32* anc = nullptr) {
     RT_DBG(5);
     if constexpr (Slots) {
         // The node walk and the triangle tests run in the same step, one leaf apart: the node walk
@@ -1061,7 +981,6 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         // next triangles are tested. Leaves are still tested in visiting order and the first leaf with
         // a hit ends the walk (a leaf the node walk found beyond it is dropped): the same result, in
         // fewer steps, with both parts of a step busy in most lanes.
-        (void)top;
         if (!w.ndone && w.nlf >= w.nle && walk_node_slots(sc, m, ray, inv, w, anc) == WALK_MISS) w.ndone = 1;
         RT_DBG_TSTART(t_lt);
         if (w.lpos < w.lend) {
@@ -1085,7 +1004,8 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
     if (w.lpos < w.lend) st = leaf_tris(sc, ray, w, t, prim);  // triangles of the open leaf
     RT_DBG_TEND(12, t_lt);
     if (st >= 0) return st;
-    st = walk_node(sc, m, ray, inv, w, top, anc);
+    (void)anc;
+    st = walk_node(sc, m, ray, inv, w);
 #if RT_WALK_OPEN_TEST
     if (st == WALK_RUN && w.lpos < w.lend) {  // a leaf was just opened: its first triangles in this step
         const int s2 = leaf_tris(sc, ray, w, t, prim);
@@ -1167,14 +1087,21 @@ RT_DEV bool mesh_hit_bvh(const DevScene& sc, const DevMesh& m, const Ray& ray, c
 }
 
 // Whole traversal in one call (megakernel / trace kernel).
-RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax, double* t,
-                     int* prim) {
+template <bool Slots>
+RT_DEV bool mesh_hit_walk(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax,
+                          double* t, int* prim) {
     OctWalk w;
-    if (!walk_begin(sc, m, ray, inv, tmax, w)) return false;
+    if (!walk_begin<Slots>(sc, m, ray, inv, tmax, w)) return false;
     int st;
-    while ((st = walk_step(sc, m, ray, inv, w, t, prim)) == WALK_RUN) {
+    while ((st = walk_step<Slots>(sc, m, ray, inv, w, t, prim)) == WALK_RUN) {
     }
     return st == WALK_HIT;
+}
+// The slot walk when the scene has its tables (DevScene::node_slot), else the node_kids walk.
+RT_DEV bool mesh_hit(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, double tmax, double* t,
+                     int* prim) {
+    if (RT_WALK_TIGHT && sc.node_slot) return mesh_hit_walk<true>(sc, m, ray, inv, tmax, t, prim);
+    return mesh_hit_walk<false>(sc, m, ray, inv, tmax, t, prim);
 }
 
 // Kernel specialisation by scene features (chosen on the host per scene/flags): code paths a

@@ -52,8 +52,7 @@ struct alignas(16) DevMesh {
     double total_weight;      // sum of triangle areas (WeightedIndex total)
     double cull_pad;          // near_box padding: 1e-7 * max(1, |box coordinates|)
     int32_t btri_base;        // first of this mesh's n_tris BVH-order triangles (DevScene::btris)
-    int32_t top_base;         // this mesh's top-levels child table in DevScene::top_kids (kTopNodes x 8
-                              // entries), or -1 (root leaf / empty octree)
+    int32_t pad5;
     int32_t root_exist;       // the root's existence mask (KidSlot): the slot walk's first walk_enter
     int32_t pad2;
     double tight_base[3], tight_step;  // KidSlot bounds: base[k] + q * step (cull box min - E, 3 E / 65535)
@@ -89,16 +88,6 @@ constexpr int32_t kKidCountEscape = 63;
 RT_LAYOUT_FN int32_t kid_leaf(int32_t leaf, int32_t first, int32_t count) {
     const bool inl = count < kKidCountEscape && first < (1 << 25);
     return -2 - ((inl ? first : leaf) << 6 | (inl ? count : kKidCountEscape));
-}
-// Top levels of an octree (depths 0..kTopDepth), indexed by position instead of node id, so a walk
-// can read them from an LDS copy without knowing the node id: the node at depth d reached through
-// octant slots o_0, o_1, .., o_{d-1} (the walk's `path`, 3 bits per level, level 0 lowest) is entry
-// top_slot(d, path); its 8 child entries are the node_kids values (kKidEmpty where no node exists).
-constexpr int kTopDepth = 3;
-constexpr int kTopNodes = 1 + 8 + 64 + 512;  // 585 nodes x 32 B = 18.3 KB
-RT_LAYOUT_FN int top_slot(int depth, uint32_t path) {
-    const int off = depth == 0 ? 0 : depth == 1 ? 1 : depth == 2 ? 9 : 73;  // (8^d - 1) / 7
-    return off + (int)(path & ((1u << (3 * depth)) - 1u));
 }
 // A walk's child pick reads one 16-byte slot: node_slot[node][8] = the child entry (as node_kids,
 // with the parent encoding below) and the child subtree's triangle
@@ -204,12 +193,12 @@ struct DevScene {
     const Bvh32* bvh32;
     const Tri32* btris32;
     const Compact32* ctab32;    // f32 compact tables (ok == 0: the generic object loop)
-    const int32_t* top_kids;    // top-levels child tables of the meshes (DevMesh::top_base)
-    const KidSlot* node_slot;   // [node][8] child entry + subtree triangle bounds (KidSlot above)
+    const KidSlot* node_slot;   // [node][8] child entry + subtree triangle bounds (KidSlot above); null
+                                // when a node id does not fit a slot entry (>= kSlotMaxNode): the walks
+                                // then read node_kids (walk_step<false>)
     const double* node_box;     // [node][6] the node's octant box (min xyz, max xyz) with the walk's own
                                 // arithmetic: a pop of the slot walk reloads the ancestor's box from here
-    int32_t top_mesh;          // the mesh whose top levels the walk-pool kernel stages in LDS, -1 none
-    int32_t top_pad;
+    int32_t pad6, pad7;
     float off32;                // f32 mode: hit points are offset by off32 * n (scene-scaled epsilon)
     int32_t n_objects, light, n_meshes, compact;
     double cam_pos[3], cam_dir[3];

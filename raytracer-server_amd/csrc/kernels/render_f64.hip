@@ -373,17 +373,24 @@ __global__ void k_selftest_arith(long n, uint64_t seed, unsigned long long* bad)
     if (e & 4) atomicAdd(&bad[2], 1ull);
 }
 
-extern "C" int rt_selftest_arith(long n, unsigned long long seed, unsigned long long out[3]) {
+// n_out: the caller's output count (at most 3 are written: reciprocal, quotient, square root)
+extern "C" int rt_selftest_arith_n(long n, unsigned long long seed, unsigned long long* out, int n_out) {
     unsigned long long* d = nullptr;
-    if (n <= 0 || hipMalloc(&d, 3 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (n <= 0 || !out || n_out <= 0 || hipMalloc(&d, 3 * sizeof(unsigned long long)) != hipSuccess) return -1;
     int rc = 0;
+    unsigned long long h[3] = {0, 0, 0};
     if (hipMemset(d, 0, 3 * sizeof(unsigned long long)) != hipSuccess) rc = -1;
     if (!rc) {
         hipLaunchKernelGGL(k_selftest_arith, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, n, seed, d);
-        if (hipGetLastError() != hipSuccess || hipMemcpy(out, d, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
+        if (hipGetLastError() != hipSuccess || hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
     }
     (void)hipFree(d);
+    for (int i = 0; i < n_out && i < 3; ++i) out[i] = h[i];
     return rc;
+}
+// The original two-output entry point (reciprocal, quotient), kept for callers built against it.
+extern "C" int rt_selftest_arith(long n, unsigned long long seed, unsigned long long out[2]) {
+    return rt_selftest_arith_n(n, seed, out, 2);
 }
 
 #define RT_DIAG_TU_FN diag_read_main

@@ -22,15 +22,14 @@ typedef __attribute__((address_space(3))) uint64_t LdsU64;
 #endif
 
 // Begins the octree walk of the next candidate mesh after gen slot g (Scene::trace_ray's /
-// mutually_visible's loop over the mesh objects); false when no mesh is left.
-// `top`: the LDS copy of mesh sc.top_mesh's top levels (walk-pool kernel), or null.
-template <class C>
+// mutually_visible's loop over the mesh objects); false when no mesh is left. S: the slot walk
+// (walk_step<true>, DevScene::node_slot) or the node_kids walk.
+template <class C, bool S>
 RT_DEV bool next_mesh_walk(const DevScene& sc, const Ray& r, const RayInv& inv, double tmax, int& g, int& mi,
-                           OctWalk& w, const LdsTopI32* top = nullptr) {
+                           OctWalk& w) {
     for (++g; g < tables(sc)->n_gen; ++g) {
         const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
-        if (o.geom == GEOM_MESH &&
-            walk_begin(sc, sc.meshes[o.mesh], r, inv, tmax, w, o.mesh == sc.top_mesh ? top : nullptr)) {
+        if (o.geom == GEOM_MESH && walk_begin<S>(sc, sc.meshes[o.mesh], r, inv, tmax, w)) {
             mi = o.mesh;
             return true;
         }
@@ -39,13 +38,12 @@ RT_DEV bool next_mesh_walk(const DevScene& sc, const Ray& r, const RayInv& inv, 
 }
 // The walk pool's form: `near` = the meshes the query's owner found near the ray (mesh_near_mask, same
 // tmax), so only those are begun, without repeating their near_box test.
-template <class C>
+template <class C, bool S>
 RT_DEV bool next_mesh_walk_near(const DevScene& sc, const Ray& r, const RayInv& inv, double tmax, int& g, int& mi,
-                                OctWalk& w, uint32_t near, const LdsTopI32* top = nullptr) {
+                                OctWalk& w, uint32_t near) {
     for (++g; g < tables(sc)->n_gen; ++g) {
         const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
-        if (o.geom == GEOM_MESH && ((near >> o.mesh) & 1u) &&
-            walk_begin(sc, sc.meshes[o.mesh], r, inv, tmax, w, o.mesh == sc.top_mesh ? top : nullptr, false)) {
+        if (o.geom == GEOM_MESH && ((near >> o.mesh) & 1u) && walk_begin<S>(sc, sc.meshes[o.mesh], r, inv, tmax, w, false)) {
             mi = o.mesh;
             return true;
         }
@@ -111,7 +109,6 @@ RT_DEV void park_load(const Park& p, WalkRegs& r) {
     r.w.order = (uint32_t)p.I(7); r.w.lpos = p.I(8); r.w.lend = p.I(9); r.w.best = p.I(10);
     r.hobj = p.I(11); r.hprim = p.I(12); r.g = p.I(13); r.mi = p.I(14); r.occluded = p.I(15);
     r.w.nlf = p.I(16); r.w.nle = p.I(17);
-    r.w.nc = kNcNone;  // the read-ahead is not parked here: the next pick reads its entry
 }
 
 // Nearest-triangle mode (Cfg::bvh): the BVH walk parks cur / sp / best / bt in the octree walk's
@@ -182,7 +179,7 @@ RT_DEV void park_query(const Park& p, const Ray& r, const RayInv& wi, double wt,
 // up to ksteps steps, after the first only while >= wmin lanes still walk. Returns, per lane,
 // whether its query finished; the results are then in pk (D16 t, I11 object, I12 prim, I15
 // occluded), otherwise the walk state is stored back into pk.
-template <class C>
+template <class C, bool S>
 RT_DEV bool walk_round(const DevScene& sc, const Park& pk, const bool wk, const bool closest, int ksteps, int wmin) {
     bool walking = wk, done = false;
     if constexpr (C::bvh) {
@@ -240,11 +237,11 @@ RT_DEV bool walk_round(const DevScene& sc, const Park& pk, const bool wk, const 
                 bool fin = false;
                 if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
                     const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
-                    fin = !next_mesh_walk<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w);
+                    fin = !next_mesh_walk<C, S>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w);
                 } else {
                     double t;
                     int prim;
-                    const int st = walk_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim);
+                    const int st = walk_step<S>(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim);
                     if (st != WALK_RUN) {
                         if (closest) {
                             if (st == WALK_HIT) {
@@ -306,7 +303,7 @@ constexpr int kPoolRefill = RT_POOL_REFILL;  // refill only when at least this m
 #define RT_PARK_INV 0  // A/B: the park keeps 1/d (1) or park2_load recomputes it (0; its 6 KB of LDS hold the
                        // pool's camera-sample buffer instead, RT_POOL_CAMBUF)
 #endif
-constexpr int kPark2D = RT_PARK_INV ? 17 : 14, kPark2I = RT_WALK_READAHEAD ? 18 : 17;
+constexpr int kPark2D = RT_PARK_INV ? 17 : 14, kPark2I = 17;
 enum : int { P2_T = 13, P2_HOBJ = 9, P2_HPRIM = 10, P2_OCC = 13, P2_NEAR = 16 };
 RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
     p.D(0) = r.wr.o.x; p.D(1) = r.wr.o.y; p.D(2) = r.wr.o.z;
@@ -324,9 +321,6 @@ RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
     p.I(5) = (int32_t)r.w.order; p.I(6) = r.w.lpos; p.I(7) = r.w.lend; p.I(8) = r.w.best;
     p.I(9) = r.hobj; p.I(10) = r.hprim; p.I(11) = r.g; p.I(12) = r.mi; p.I(13) = r.occluded;
     p.I(14) = r.w.nlf; p.I(15) = r.w.nle;
-#if RT_WALK_READAHEAD
-    p.I(17) = r.w.nc;
-#endif
 }
 RT_DEV void park2_load(const Park& p, WalkRegs& r) {
     r.wr.o = v3(p.D(0), p.D(1), p.D(2));
@@ -348,11 +342,6 @@ RT_DEV void park2_load(const Park& p, WalkRegs& r) {
     r.w.order = (uint32_t)p.I(5); r.w.lpos = p.I(6); r.w.lend = p.I(7); r.w.best = p.I(8);
     r.hobj = p.I(9); r.hprim = p.I(10); r.g = p.I(11); r.mi = p.I(12); r.occluded = p.I(13);
     r.w.nlf = p.I(14); r.w.nle = p.I(15);
-#if RT_WALK_READAHEAD
-    r.w.nc = p.I(17);  // its child entries are loaded again by walk_reload_ahead
-#else
-    r.w.nc = kNcNone;
-#endif
 }
 // A new pool query (see park_query); near: the meshes near the ray (mesh_near_mask).
 RT_DEV void park2_query(const Park& p, const Ray& r, const RayInv& wi, double wt, int32_t hobj, int32_t hprim,
@@ -368,17 +357,14 @@ RT_DEV void park2_query(const Park& p, const Ray& r, const RayInv& wi, double wt
     p.D(13) = wt;
     p.I(0) = -1;
     p.I(9) = hobj; p.I(10) = hprim; p.I(11) = -1; p.I(13) = 0;
-#if RT_WALK_READAHEAD
-    p.I(17) = kNcNone;
-#endif
 }
 
 // One pool round: up to ksteps walk steps over queries taken from the pool; a lane whose query
 // finishes hands the result to its owner and, while steps remain, takes the next queued query
 // (refill: the round keeps its lanes full). Unfinished queries go back to the pool. All lanes call.
-template <class C>
+template <class C, bool S>
 RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d, LdsInt* park_i, int need,
-                       int ksteps, const LdsTopI32* top) {
+                       int ksteps) {
     RT_DBG_TSTART(t_tk);
     int32_t q = queue_take(wp.q, need);
     if (!__any(q >= 0)) {
@@ -390,7 +376,6 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
     auto col = [&](int32_t c) { return Park{park_d + c, park_i + c}; };
     if (q >= 0) {
         park2_load(col(q), r);
-        if (r.w.cur >= 0) walk_reload_ahead(sc, r.w, r.mi == sc.top_mesh ? top : nullptr);
         const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         closest = stq == POOL_CLOSEST;
         if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
@@ -404,15 +389,15 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
             if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
                 RT_DBG_TSTART(t_bg);
                 const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
-                fin = !next_mesh_walk_near<C>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, (uint32_t)col(q).I(P2_NEAR), top);
+                fin = !next_mesh_walk_near<C, S>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, (uint32_t)col(q).I(P2_NEAR));
                 RT_DBG_TEND(15, t_bg);
             }
             // (a walk begun above takes its first step right away: the slot walk enters the root there)
             if (!fin && r.w.cur >= 0) {
                 double t;
                 int prim;
-                const int st = walk_step(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim, r.mi == sc.top_mesh ? top : nullptr,
-                                         (LdsInt*)park_i + kPark2I * kParkThreads + q);
+                const int st = walk_step<S>(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim,
+                                            S ? (LdsAncI32*)park_i + kPark2I * kParkThreads + q : nullptr);
                 if (st != WALK_RUN) {
                     if (closest) {
                         if (st == WALK_HIT) {
@@ -445,7 +430,6 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
             if (q2 >= 0) {
                 q = q2;
                 park2_load(col(q), r);
-        if (r.w.cur >= 0) walk_reload_ahead(sc, r.w, r.mi == sc.top_mesh ? top : nullptr);
                 const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 closest = stq == POOL_CLOSEST;
                 if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
@@ -459,7 +443,7 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
     return true;
 }
 
-template <int F, int W, int P>
+template <int F, int W, int P, bool S>
 __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
                                                                uint32_t* next_sub, long nsub, int ksteps, int wmin,
                                                                int refill, int pool_min, int pool_vmin) {
@@ -479,8 +463,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     }
 #endif
     __shared__ double s_park_d[(P ? kPark2D : kParkD) * kParkThreads];
-    // pool: + ancestor ids (walk_node / walk_node_slots)
-    __shared__ int32_t s_park_i[(P ? kPark2I + (RT_WALK_TIGHT ? kSlotAncLevels : kAncLevels) : kParkI) * kParkThreads];
+    // pool: + the slot walk's ancestor ids (walk_node_slots)
+    __shared__ int32_t s_park_i[(P ? kPark2I + (S ? kSlotAncLevels : 0) : kParkI) * kParkThreads];
     const Park park{(LdsDouble*)s_park_d + threadIdx.x, (LdsInt*)s_park_i + threadIdx.x};
     // P = 1: one walk queue
     __shared__ int32_t s_ring[1][P ? 256 : 1];
@@ -489,19 +473,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     WalkPool wp;
     wp.q = LdsQueue{s_ring[0], s_qhead, s_qtail, 255u};
     wp.status = s_status;
-    // pool: the top kTopDepth + 1 levels of the deepest mesh's octree in LDS (18.3 KB; the walks of
-    // every query of the block start there), scene_layout.h: top_slot
-    // (the slot walk, RT_WALK_TIGHT, reads every level through the node slots: no LDS copy)
-    __shared__ int4 s_top[P && !RT_WALK_TIGHT ? kTopNodes * 2 : 1];
-    const LdsTopI32* top = nullptr;
     if constexpr (P) {
         s_ring[0][threadIdx.x] = -1;
         if (threadIdx.x < 2) { s_qhead[threadIdx.x] = 0; s_qtail[threadIdx.x] = 0; }
-        if (!RT_WALK_TIGHT && sc.top_mesh >= 0) {
-            const int4* src = reinterpret_cast<const int4*>(sc.top_kids + sc.meshes[sc.top_mesh].top_base);
-            for (int i = threadIdx.x; i < kTopNodes * 2; i += blockDim.x) s_top[i] = src[i];
-            top = (const LdsTopI32*)(LdsInt*)s_top;
-        }
         __syncthreads();
     }
     // subpixel accumulator and camera-sample buffer in LDS, as in k_megakernel_f64 (pool mode: the
@@ -539,14 +513,14 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
         if constexpr (P) {
             // take queued queries (at least pool_min of them while this wave has paths to shade)
             const int ready = __popcll(__ballot(active && !walking));
-            took = pool_round<C>(sc, wp, (LdsDouble*)s_park_d, (LdsInt*)s_park_i, ready ? pool_min : 1, ksteps, top);
+            took = pool_round<C, S>(sc, wp, (LdsDouble*)s_park_d, (LdsInt*)s_park_i, ready ? pool_min : 1, ksteps);
             if (!took && !ready) {
                 __builtin_amdgcn_s_sleep(2);  // every path of this wave waits on walks other waves hold
             }
             if (walking && __hip_atomic_load(&s_status[threadIdx.x], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == POOL_DONE)
                 walking = false;
         } else if (__any(walking)) {
-            if (walk_round<C>(sc, park, walking, phase == PH_WALK_CLOSEST, ksteps, wmin)) walking = false;
+            if (walk_round<C, S>(sc, park, walking, phase == PH_WALK_CLOSEST, ksteps, wmin)) walking = false;
         }
         RT_DBG_TEND(1, t_wk);
         RT_DBG_TSTART(t_vx);
@@ -769,20 +743,21 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     RT_DBG_TFLUSH();
 }
 
-template <int F, int W, int P>
+template <int F, int W, int P, bool S = (RT_WALK_TIGHT != 0)>
 static void launch_mm(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub, long nsub,
                       int ksteps, int wmin, int refill, int pool_min, int pool_vmin, double* tail_buf, size_t tail_cap,
                       hipStream_t st) {
-    const long blocks = resident_blocks(k_megakernel_mesh_f64<F, W, P>, (nsub + 255) / 256);
+    const long blocks = resident_blocks(k_megakernel_mesh_f64<F, W, P, S>, (nsub + 255) / 256);
     RenderArgs a = a_in;
     plan_tail(a, nsub, blocks * 256, tail_buf, tail_cap);
-    hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W, P>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf,
+    hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W, P, S>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf,
                        next_sub, nsub, ksteps, wmin, refill, pool_min, pool_vmin);
     launch_tail_sum_f64(a, sub_buf, nsub - a.n_whole, st);
 }
 
-// Octree walks through the block's walk pool, 2 waves/SIMD (RT_MK_POOL=3: 3 waves/SIMD, 37 spilled
-// VGPRs, measured 6% slower; 0: each lane walks its own query, RT_MK_KSTEPS steps per iteration).
+// Octree walks through the block's walk pool, 2 waves/SIMD (3 waves/SIMD: 37 spilled VGPRs, measured 6%
+// slower; RT_MK_POOL=0: each lane walks its own query, RT_MK_KSTEPS steps per iteration).
+// Scenes without slot tables (DevScene::node_slot null: node ids >= kSlotMaxNode) walk node_kids.
 hipError_t launch_megakernel_mesh_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
                                       long nsub, int refill, int wmin, double* tail_buf, size_t tail_cap, hipStream_t st) {
     static const int ksteps = std::max(1, env_int("RT_MK_KSTEPS", 4));
@@ -793,7 +768,7 @@ hipError_t launch_megakernel_mesh_f64(const DevScene& sc, const RenderArgs& a, d
     static const int pool_refill = env_int("RT_MK_POOL_CAM_REFILL", 20);  // the walk pool's camera refill threshold
 #define RT_MM_CASE(F)                                                                          \
     case F:                                                                                    \
-        if (pool == 3) launch_mm<F, 3, 1>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, pool_refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
+        if (!sc.node_slot) launch_mm<F, 2, 1, false>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, pool_refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
         else if (pool) launch_mm<F, 2, 1>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, pool_refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
         else launch_mm<F, 2, 0>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, 0, 0, tail_buf, tail_cap, st); \
         break;

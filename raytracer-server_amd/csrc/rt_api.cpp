@@ -7,7 +7,6 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
-#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -57,8 +56,8 @@ struct Packed {
     std::vector<rt::DevBvhNode> bvh;  // nearest-triangle mode (RT_FLAG_MESH_NEAREST)
     std::vector<rt::DevTri> btris;
     std::vector<int32_t> btri_id;
-    std::vector<int32_t> top_kids;  // [mesh tables][kTopNodes][8]: octree top levels by position (top_slot)
-    std::vector<rt::KidSlot> slots;      // [node][8] child entry + subtree triangle bounds (scene_layout.h KidSlot)
+    std::vector<rt::KidSlot> slots;      // [node][8] child entry + subtree triangle bounds (scene_layout.h KidSlot);
+                                         // empty when a node id does not fit a slot entry (the node_kids walk)
     std::vector<double> node_box;        // [node][6] octant boxes, the walk's arithmetic (DevScene::node_box)
 };
 
@@ -248,11 +247,18 @@ void build_bvh(Packed& p, const rt::host::Mesh& m, int32_t tri_base) {
     if (n > 0) rec.build(0, n, 0);
 }
 
-// RT_OK, or RT_E_INVAL when the octree tables cannot encode the mesh (kid_leaf: leaf ids < 2^25).
+// RT_OK, or RT_E_INVAL when the octree tables cannot encode the mesh (kid_leaf: leaf ids < 2^25). Node ids
+// beyond a KidSlot entry's range (>= kSlotMaxNode, global over the scene's meshes) leave the scene without
+// slot tables: its walks then read node_kids (walk_step<false>, the same result without the subtree culls).
 int pack_scene(rt_scene* s) {
     using namespace rt::host;
     Packed& p = s->packed;
     const Scene& sc = s->host;
+    bool slots_ok = true;
+    // RT_SLOT_MAX_NODE (tests): a lower node-id limit for the slot tables, down to 0 = none (the node_kids
+    // walk for every scene); the encoding itself holds ids below kSlotMaxNode
+    int32_t slot_max = rt::kSlotMaxNode;
+    if (const char* v = std::getenv("RT_SLOT_MAX_NODE")) slot_max = std::max(0, std::min(slot_max, std::atoi(v)));
     for (const Mesh& m : sc.meshes) {
         rt::DevMesh dm{};
         dm.node_base = (int32_t)p.up.size();
@@ -451,9 +457,8 @@ int pack_scene(rt_scene* s) {
                             b[3 + q] = sb[6 * (size_t)c8 + 3 + q] + dm.cull_pad;
                         }
                     int32_t e = p.kids[8 * (j + (size_t)dm.node_base) + k];
+                    if (e >= slot_max) slots_ok = false;  // checked after the loop: no slot tables
                     if (e >= 0) {  // a parent: its node id and its own existence mask (KidSlot)
-                        if (e >= rt::kSlotMaxNode)
-                            return fail(RT_E_INVAL, "mesh octree too large: node ids must stay below 2^23 (scene_layout.h KidSlot)");
                         uint32_t ex = 0;
                         for (int q = 0; q < 8; ++q) ex |= (oc.child[8 * (size_t)c8 + q] >= 0 ? 1u : 0u) << q;
                         e = rt::slot_parent(e, ex);
@@ -462,24 +467,9 @@ int pack_scene(rt_scene* s) {
                 }
             }
         }
-        // top levels (depths 0..kTopDepth) by position: what the walk-pool kernel stages in LDS
-        dm.top_base = -1;
-        if (oc.size() > 0 && !oc.kind[0]) {
-            dm.top_base = (int32_t)p.top_kids.size();
-            p.top_kids.resize(p.top_kids.size() + (size_t)rt::kTopNodes * 8, rt::kKidEmpty);
-            int32_t* top = p.top_kids.data() + dm.top_base;
-            std::function<void(int32_t, int, uint32_t)> fill = [&](int32_t node, int depth, uint32_t path) {
-                const int slot = rt::top_slot(depth, path);
-                for (int k = 0; k < 8; ++k) {
-                    const int32_t e = p.kids[8 * (size_t)node + k];
-                    top[8 * slot + k] = e;
-                    if (e >= 0 && depth < rt::kTopDepth) fill(e, depth + 1, path | (uint32_t)k << (3 * depth));
-                }
-            };
-            fill(dm.node_base, 0, 0u);
-        }
         p.meshes.push_back(dm);
     }
+    if (!slots_ok) p.slots.clear();
     for (const Object& o : sc.objects) {
         rt::DevObject d{};
         d.geom = o.geom;
@@ -686,8 +676,7 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         put(blob, &o_obj32, obj32);
         put(blob, &o_bvh32, bvh32);
         put(blob, &o_tri32, tri32);
-        size_t o_top, o_slot;
-        put(blob, &o_top, p.top_kids);
+        size_t o_slot;
         put(blob, &o_slot, p.slots);
         size_t o_nbox;
         put(blob, &o_nbox, p.node_box);
@@ -720,20 +709,8 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.off32 = off32;
         ds.ctab32 = (const rt::Compact32*)(b + o_tab32);
         ds.compact = compact;
-        // the walk-pool kernel stages the top levels of the largest octree in LDS (RT_MK_TOP=0: off, A/B)
-        ds.top_kids = (const int32_t*)(b + o_top);
-        ds.node_slot = (const rt::KidSlot*)(b + o_slot);
+        ds.node_slot = p.slots.empty() ? nullptr : (const rt::KidSlot*)(b + o_slot);
         ds.node_box = (const double*)(b + o_nbox);
-        ds.top_mesh = -1;
-        const char* top_env = std::getenv("RT_MK_TOP");
-        if (!(top_env && std::atoi(top_env) == 0)) {
-            int32_t most = 0;
-            for (size_t i = 0; i < p.meshes.size(); ++i)
-                if (p.meshes[i].top_base >= 0 && p.meshes[i].n_nodes > most) {
-                    most = p.meshes[i].n_nodes;
-                    ds.top_mesh = (int32_t)i;
-                }
-        }
         ds.light = s->host.light;
         ds.light_pdf = 0.0;
         if (ds.light >= 0 && ds.light < (int32_t)p.objects.size()) {
@@ -826,6 +803,21 @@ void give_workspace(rt_scene* s, std::unique_ptr<rt::Workspace> w, hipStream_t s
 // (RenderArgs::cancel) between subpixels. The caller's flag itself is never registered with HIP (it
 // may be shared by concurrent renders, or sit on memory HIP cannot pin): the host thread that waits
 // for the render copies it into the mirror (wait_stream), so its lifetime stays the caller's.
+// The words come from a process-wide free list and go back to it once the render has drained: a
+// cancellable render (the WebSocket server renders chunk by chunk with a flag) costs no pinned
+// allocation after the first. The words are never freed (one per concurrently cancellable render).
+struct CancelWord {
+    int32_t* host;
+    int32_t* dev;
+};
+struct CancelWordPool {
+    std::mutex mu;
+    std::vector<CancelWord> free;
+};
+CancelWordPool& cancel_words() {
+    static CancelWordPool* pool = new CancelWordPool;  // never destroyed: no HIP calls at process teardown
+    return *pool;
+}
 struct CancelMirror {
     int32_t* host = nullptr;
     int32_t* dev = nullptr;
@@ -833,19 +825,39 @@ struct CancelMirror {
     CancelMirror(const CancelMirror&) = delete;
     CancelMirror& operator=(const CancelMirror&) = delete;
     ~CancelMirror() {
-        if (host) (void)hipHostFree(host);
+        if (!host) return;
+        CancelWordPool& p = cancel_words();
+        std::lock_guard<std::mutex> lk(p.mu);
+        p.free.push_back(CancelWord{host, dev});
     }
     hipError_t init() {
-        // coherent (fine-grained): hipHostMalloc's default is non-coherent memory the GPU may cache, so
-        // a host write could stay invisible to the polling kernel until the line is evicted
-        hipError_t e = hipHostMalloc((void**)&host, sizeof(int32_t),
-                                     hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
-        if (e != hipSuccess) {
-            host = nullptr;
-            return e;
+        {
+            CancelWordPool& p = cancel_words();
+            std::lock_guard<std::mutex> lk(p.mu);
+            if (!p.free.empty()) {
+                host = p.free.back().host;
+                dev = p.free.back().dev;
+                p.free.pop_back();
+            }
         }
-        *(volatile int32_t*)host = 0;
-        return hipHostGetDevicePointer((void**)&dev, host, 0);
+        if (!host) {
+            // coherent (fine-grained): hipHostMalloc's default is non-coherent memory the GPU may cache, so
+            // a host write could stay invisible to the polling kernel until the line is evicted
+            hipError_t e = hipHostMalloc((void**)&host, sizeof(int32_t),
+                                         hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
+            if (e != hipSuccess) {
+                host = nullptr;
+                return e;
+            }
+            e = hipHostGetDevicePointer((void**)&dev, host, 0);
+            if (e != hipSuccess) {
+                (void)hipHostFree(host);
+                host = nullptr;
+                return e;
+            }
+        }
+        __atomic_store_n(host, 0, __ATOMIC_RELEASE);
+        return hipSuccess;
     }
     void raise() {
         if (host) __atomic_store_n(host, 1, __ATOMIC_RELEASE);
@@ -853,20 +865,26 @@ struct CancelMirror {
 };
 
 // Waits for everything enqueued on `st`, copying the caller's cancel flag into the mirror meanwhile.
+// Polls with a growing pause (10 us doubling to 200 us), so a short render (one WebSocket chunk) is
+// seen done within about its own duration.
 hipError_t wait_stream(hipStream_t st, const volatile int32_t* cancel, CancelMirror* mirror) {
     if (!cancel || !mirror || !mirror->host) return hipStreamSynchronize(st);
+    int us = 10;
     for (;;) {
         const hipError_t e = hipStreamQuery(st);
         if (e != hipErrorNotReady) return e;
         if (*cancel) mirror->raise();
-        std::this_thread::sleep_for(std::chrono::microseconds(200));
+        std::this_thread::sleep_for(std::chrono::microseconds(us));
+        us = std::min(200, 2 * us);
     }
 }
 
 // Statistics of an enqueued megakernel render, completed once its stream has drained (finish): the
 // render's HIP events and a pinned copy of the workspace's vertex counter (copied on the stream
 // before the workspace goes back to the pool). Nothing here synchronises, so callers can keep several
-// renders in flight (rt_render_multi) and still collect their stats.
+// renders in flight (rt_render_multi) and still collect their stats. The events and the pinned word
+// are made by the first init and reused by later ones (rt_render_multi: one PendingStats per band
+// slot of a worker), and freed only when the object goes (after its renders have drained).
 struct PendingStats {
     rt_render_stats* out = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -876,20 +894,19 @@ struct PendingStats {
     PendingStats() = default;
     PendingStats(const PendingStats&) = delete;
     PendingStats& operator=(const PendingStats&) = delete;
-    ~PendingStats() { release(); }
-    void release() {
+    ~PendingStats() {
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         if (count) (void)hipHostFree(count);
-        e0 = e1 = nullptr;
-        count = nullptr;
     }
     hipError_t init(rt_render_stats* o) {
         out = o;
         std::memset(out, 0, sizeof *out);
-        hipError_t e = hipEventCreate(&e0);
-        if (e == hipSuccess) e = hipEventCreate(&e1);
-        if (e == hipSuccess) e = hipHostMalloc((void**)&count, sizeof(unsigned long long), hipHostMallocDefault);
+        device_done = false;
+        hipError_t e = hipSuccess;
+        if (!e0) e = hipEventCreate(&e0);
+        if (e == hipSuccess && !e1) e = hipEventCreate(&e1);
+        if (e == hipSuccess && !count) e = hipHostMalloc((void**)&count, sizeof(unsigned long long), hipHostMallocDefault);
         if (e == hipSuccess) *count = 0;
         return e;
     }
@@ -909,7 +926,6 @@ struct PendingStats {
             out->vertices = (int64_t)*count;
         }
         out->samples = samples;
-        release();
         return RT_OK;
     }
 };
@@ -1091,6 +1107,7 @@ int rt_scene_info(const rt_scene* s, int64_t info[16]) {
         if (m.octree.max_leaf > info[9]) info[9] = m.octree.max_leaf;
         if (m.octree.max_depth > info[10]) info[10] = m.octree.max_depth;
     }
+    info[11] = s->packed.slots.empty() ? 0 : 1;
     return RT_OK;
 }
 
@@ -1217,9 +1234,16 @@ int rt_render_multi(const rt_scene* scene, const rt_render_params* p, const int3
     int rc = check_params(p);
     if (rc != RT_OK) return rc;
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RT_E_NODEVICE, "no HIP device");
+    if (hipGetDeviceCount(&ndev) != hipSuccess) {
+        (void)hipGetLastError();
+        ndev = 0;
+    }
+    // an ordinal no visible device has is the caller's error (RT_E_INVAL), checked before anything runs;
+    // with no device at all every ordinal is out of range
     for (int32_t i = 0; i < n_devices; ++i)
-        if (devices[i] < 0 || devices[i] >= ndev) return fail(RT_E_INVAL, "device ordinal out of range");
+        if (devices[i] < 0 || devices[i] >= ndev)
+            return fail(RT_E_INVAL, "device ordinal " + std::to_string(devices[i]) + " out of range (" +
+                                        std::to_string(ndev) + " HIP devices visible)");
     const int32_t tw = p->tile_w, th = p->tile_h;
     if ((size_t)tw * th == 0) return RT_OK;
     const int32_t nb = rt_band_plan(th, n_devices, band_rows, 0, nullptr, nullptr);

@@ -108,6 +108,8 @@ def _load():
     # diagnostics (include/rt_diag.h)
     if hasattr(L, "rt_selftest_arith"):  # absent from libraries built before it existed (A/B variants)
         L.rt_selftest_arith.argtypes = [ctypes.c_long, ctypes.c_ulonglong, P(ctypes.c_ulonglong)]
+    if hasattr(L, "rt_selftest_arith_n"):
+        L.rt_selftest_arith_n.argtypes = [ctypes.c_long, ctypes.c_ulonglong, P(ctypes.c_ulonglong), ctypes.c_int]
     if hasattr(L, "rt_debug_qcheck"):
         L.rt_debug_qcheck.argtypes = [P(ctypes.c_ulonglong)]
     if hasattr(L, "rt_debug_counters"):
@@ -207,7 +209,7 @@ class Scene:
         a = np.zeros(16, dtype=np.int64)
         _check(lib.rt_scene_info(self._h, _ptr(a, ctypes.c_int64)))
         keys = ["objects", "light", "meshes", "nodes", "parents", "leaves", "refs", "triangles", "vertices",
-                "max_leaf", "max_depth"]
+                "max_leaf", "max_depth", "slot_tables"]
         return {k: int(a[i]) for i, k in enumerate(keys)}
 
     def mesh(self, obj):
@@ -351,7 +353,7 @@ class RenderJob:
 def selftest_arith(n=1 << 24, seed=0x5EED):
     """Device check of the exact-arithmetic shortcuts: (reciprocal, quotient, square-root mismatches)."""
     out = (ctypes.c_ulonglong * 3)()
-    _check(lib.rt_selftest_arith(n, seed, out))
+    _check(lib.rt_selftest_arith_n(n, seed, out, 3))
     return int(out[0]), int(out[1]), int(out[2])
 
 

@@ -26,7 +26,8 @@ def test_exports_every_declared_symbol(rt):
 def test_exports_diagnostics(rt):
     text = open(os.path.join(REPO, "include", "rt_diag.h")).read()
     names = re.findall(r"^int\s+(rt_[a-z_0-9]+)\s*\(", text, re.M)
-    assert names == ["rt_selftest_arith", "rt_debug_qcheck", "rt_debug_counters", "rt_debug_regions"]
+    assert names == ["rt_selftest_arith_n", "rt_selftest_arith", "rt_debug_qcheck", "rt_debug_counters",
+                     "rt_debug_regions"]
     for n in names:
         assert hasattr(rt.lib, n), f"missing export {n}"
     assert rt.debug_qcheck() is None  # the product library is built without the protocol checks
@@ -52,6 +53,34 @@ def test_errors_are_codes_not_crashes(rt):
     assert rt.lib.rt_scene_load_toml(b"/nonexistent.toml", None, ctypes.byref(h)) == -4
     assert b"nonexistent" in rt.lib.rt_last_error()
     assert rt.lib.rt_render(None, None, None, None, None, None) == -1
+
+
+def test_render_multi_rejects_bad_device_ordinals(rt):
+    """rt_render_multi checks every device ordinal against the visible HIP devices before it starts
+    a worker: an ordinal no device has (negative, or >= the device count; on a host without a GPU
+    every ordinal) is RT_E_INVAL with a message, never a crash."""
+    from conftest import scene_path
+
+    sc = rt.Scene.from_toml(scene_path("cornell_box"))
+    p = rt.make_params(64, 48, 4, 1, (0, 0, 64, 48), rt.FLAG_MEGAKERNEL, 0, 1)
+    out = (ctypes.c_uint8 * (64 * 48 * 3))()
+    n = rt.lib.rt_device_count()
+    for bad in (-1, n, n + 7, 1 << 30):
+        devs = (ctypes.c_int32 * 2)(0, bad)
+        assert rt.lib.rt_render_multi(sc.handle, ctypes.byref(p), devs, 2, 0, out, None, None) == -1
+        assert b"out of range" in rt.lib.rt_last_error()
+
+
+def test_scene_without_slot_tables_still_loads(rt, monkeypatch):
+    """An octree whose node ids exceed the child-slot encoding loads without its slot tables (rt_scene_info
+    [11] = 0) instead of failing; RT_SLOT_MAX_NODE lowers the limit to stand in for a 2^23-node mesh.
+    (The GPU test test_walk_culls_do_not_change_frames renders such a scene.)"""
+    from conftest import scene_path
+
+    assert rt.Scene.from_toml(scene_path("flying_unicorn")).info()["slot_tables"] == 1
+    monkeypatch.setenv("RT_SLOT_MAX_NODE", "1000")
+    info = rt.Scene.from_toml(scene_path("flying_unicorn")).info()
+    assert info["nodes"] == 47183 and info["slot_tables"] == 0
 
 
 def test_band_plan_covers_tile_in_order(rt):

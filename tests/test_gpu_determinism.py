@@ -108,12 +108,12 @@ print(json.dumps(out))
 """
 
 
-@pytest.mark.parametrize("env", [{"RT_MK_FPOOL": "0"}, {"RT_MK_POOL": "0"}, {"RT_MK_POOL": "3"}, {"RT_MK_NOSPEC": "0"},
+@pytest.mark.parametrize("env", [{"RT_MK_FPOOL": "0"}, {"RT_MK_POOL": "0"}, {"RT_MK_NOSPEC": "0"},
                                  {"RT_MK_FPOOL_REFILL": "0", "RT_MK_POOL_CAM_REFILL": "0"}])
 def test_kernel_variants_render_the_default_frames(env):
     """The A/B kernel variants behind RT_* switches (read once per process, so each in a subprocess):
     the block-synchronous flat kernel (RT_MK_FPOOL=0), per-lane octree walks (RT_MK_POOL=0), the
-    walk pool at 3 waves/SIMD (RT_MK_POOL=3), the mirror-capable query-pool instance on the mirror-free
+    mirror-capable query-pool instance on the mirror-free
     cubes (RT_MK_NOSPEC=0: the default runs Cfg bit 32) and both pools without their camera-sample
     refill pass render byte-identical frames to the defaults."""
     base = dict(os.environ, RT_REPO=REPO)
@@ -126,3 +126,51 @@ def test_kernel_variants_render_the_default_frames(env):
         assert out.returncode == 0, out.stderr[-3000:]
         runs.append(json.loads(out.stdout.strip().splitlines()[-1]))
     assert runs[0] == runs[1], (env, runs)
+
+
+# C3 / C4 at their full 1920x1080 (reduced spp): one render per scene, frame digests as JSON
+_CULL_SCRIPT = """
+import hashlib, json, os, sys
+sys.path.insert(0, os.path.join(os.environ["RT_REPO"], "raytracer-server_amd"))
+import rt_amd
+out = {}
+for name in ("cubes", "flying_unicorn"):
+    s = rt_amd.Scene.from_toml(os.path.join(os.environ["RT_REPO"], "scenes", name + ".toml"))
+    out[name + "/slots"] = s.info()["slot_tables"]
+    out[name] = hashlib.sha1(rt_amd.render(s, 1920, 1080, 8, 0x5EED, megakernel=True)[0].tobytes()).hexdigest()[:12]
+print(json.dumps(out))
+"""
+_cull_frames = {}
+
+
+def _cull_run(lib=None, env=None):
+    e = {k: v for k, v in os.environ.items() if k not in ("RT_SLOT_MAX_NODE", "RT_AMD_LIB")}
+    e.update(RT_REPO=REPO, **(env or {}))
+    if lib:
+        e["RT_AMD_LIB"] = lib
+    out = subprocess.run([sys.executable, "-c", _CULL_SCRIPT], env=e, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("variant", ["walkref", "near64", "noslots"])
+def test_walk_culls_do_not_change_frames(variant):
+    """The culls the mesh kernels add to the reference's octree walk (geometry.rs:1262-1273) are exact:
+    the cubes (C3) and the unicorn (C4) at 1920x1080 render byte-identical frames without them —
+      walkref: the octree walked in the reference's visiting order with no subtree-bounds culls
+               (-DRT_WALK_TIGHT=0, lib/variants/walkref.so: node_kids walks);
+      near64:  the per-mesh near tests in f64 (near_box) instead of f32 (near_mesh32), -DRT_NEAR32=0;
+      noslots: the default library on a scene loaded without its slot tables (RT_SLOT_MAX_NODE=0, the
+               path a 2^23-node octree takes: the pool kernel's node_kids instance)."""
+    if "default" not in _cull_frames:
+        _cull_frames["default"] = _cull_run()
+    base = _cull_frames["default"]
+    assert base["cubes/slots"] == 1 and base["flying_unicorn/slots"] == 1
+    if variant == "noslots":
+        got = _cull_run(env={"RT_SLOT_MAX_NODE": "0"})
+        assert got["flying_unicorn/slots"] == 0 and got["cubes/slots"] == 0
+    else:
+        lib = os.path.join(REPO, "raytracer-server_amd", "lib", "variants", variant + ".so")
+        assert os.path.exists(lib), f"{lib} not built (make -C raytracer-server_amd variants)"
+        got = _cull_run(lib=lib)
+    assert got["cubes"] == base["cubes"] and got["flying_unicorn"] == base["flying_unicorn"], (variant, base, got)

@@ -355,24 +355,11 @@ def test_extra_assets_parity(asset, rt, oracle, tmp_path):
     _assert_fp32_stats(sub_f, sub_d, rgb_f, rgb_d, f"{asset}/f32")
 
 
-def test_octree_top_levels_in_lds_same_frame(rt, monkeypatch):
-    """The walk pool reading the octree's depths 0..3 from its LDS copy (top_slot: indexed by the
-    walk's octant path) gives the frame of the walk reading node_kids (RT_MK_TOP=0, read at upload)."""
-    from conftest import scene_path
-
-    w, h, spp = 96, 64, 8
-    on = rt.Scene.from_toml(scene_path("flying_unicorn"))
-    a, sa, _ = rt.render(on, w, h, spp, SEED, megakernel=True, want_sub=True)
-    monkeypatch.setenv("RT_MK_TOP", "0")
-    off = rt.Scene.from_toml(scene_path("flying_unicorn"))
-    b, sb, _ = rt.render(off, w, h, spp, SEED, megakernel=True, want_sub=True)
-    assert np.array_equal(a, b) and np.array_equal(sa, sb)
-
-
 def test_two_deep_meshes_parity(rt, oracle, tmp_path):
-    """Two deep octrees in one scene (chair.obj and crewmate.obj side by side): the walk-pool kernel
-    stages the larger octree's top levels in LDS (DevScene::top_mesh) and walks the other from
-    node_kids; megakernel and wavefront against the oracle at the 1e-9 / RGB8 bounds."""
+    """Two deep octrees in one scene (chair.obj and crewmate.obj side by side): the walk pool takes
+    queries that walk both meshes (a query's walks of the two octrees run one after the other, in the
+    scene's object order, with the reference's tie rule between their hits); megakernel and wavefront
+    against the oracle at the 1e-9 / RGB8 bounds."""
     import os
     from test_host_prep import EXTRA_ASSET_SCENE, REPO
 
