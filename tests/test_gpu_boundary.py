@@ -82,6 +82,16 @@ def test_render_multi_equals_render(name, rt, gpu_scenes):
     assert np.array_equal(got, want)
 
 
+def test_render_multi_rejects_missing_device(rt, gpu_scenes):
+    """An ordinal past the visible devices (here: device_count()) fails the whole call with RT_E_INVAL
+    before any band runs, and the next call renders normally."""
+    n = rt.device_count()
+    with pytest.raises(rt.RtError, match="out of range"):
+        rt.render_multi(gpu_scenes["cornell_box"], 64, 48, 4, [0, n], SEED)
+    rgb, st = rt.render_multi(gpu_scenes["cornell_box"], 64, 48, 4, [0], SEED)
+    assert st["samples"] == 64 * 48 * 4 and rgb.any()
+
+
 def test_render_multi_cancel(rt, gpu_scenes):
     flag = ctypes.c_int32(0)
     timer = threading.Timer(0.3, lambda: setattr(flag, "value", 1))

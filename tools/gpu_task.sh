@@ -6,6 +6,8 @@
 #   tests:EXPR       the same with -k EXPR
 #   smoke            __graft_entry__.smoke()
 #   bench            python bench.py (headline line, cpu_baseline included)
+#   rehearse[:N]     the N-rank bench path (default 2) on this one GPU: torchrun, every rank on GPU 0
+#                    (RT_BENCH_DEVICE=0), 1 step; its frame_sha1 must equal N = 1's
 #   trace            rocprofv3 --kernel-trace --stats of `python bench.py --no-cpu-baseline`
 #   benchpmc         counter passes over `bench.py --steps 1 --warmup 0`: HBM bytes -> $OUT/pmc_traffic.json,
 #                    VALU mix + clock -> $OUT/pmc_valu.json (bench.py roofline.traffic / .compute)
@@ -53,6 +55,12 @@ for task in "$@"; do
     bench)
         timeout -k 10 600 python bench.py $BENCH_ARGS > "$OUT/bench.log" 2>&1 || fail bench "$OUT/bench.log"
         tail -1 "$OUT/bench.log" ;;
+    rehearse)
+        n=${A[1]:-2}
+        RT_BENCH_DEVICE=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
+            --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus "$n" --steps 1 --warmup 0 $BENCH_ARGS \
+            > "$OUT/rehearsal_n$n.log" 2>&1 || fail rehearse "$OUT/rehearsal_n$n.log"
+        grep '^{"metric"' "$OUT/rehearsal_n$n.log" | tail -1 | cut -c1-400 ;;
     trace)
         timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
             python bench.py --no-cpu-baseline $BENCH_ARGS > "$OUT/trace.log" 2>&1 || fail trace "$OUT/trace.log"
