@@ -778,6 +778,7 @@ constexpr int kSlotAncLevels = 9;
 #ifndef RT_SLOT_CULL
 #define RT_SLOT_CULL 1  // A/B: 0 = the slot walk without the subtree-bounds test
 #endif  // the deepest parents sit at depth 8 (MAX_DEPTH 10, root depth 1)
+template <int AS = 256>  // `anc`'s stride (the block's threads)
 RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w,
                            LdsAncI32* anc = nullptr) {
     RT_DBG_TSTART(t_pop);
@@ -798,7 +799,7 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
             return WALK_MISS;
         }
         if (anc) {
-            w.cur = anc[lv * 256];
+            w.cur = anc[lv * AS];
         } else {
             int32_t cur = w.cur;
             for (int l = w.depth; l > lv; --l) cur = sc.node_up[cur].x;
@@ -874,7 +875,7 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
     }
     // descend: push the remaining mask of `cur`, take the octant's box
     const int lv = w.depth;
-    if (anc) anc[lv * 256] = w.cur;
+    if (anc) anc[lv * AS] = w.cur;
     if (lv < 8) w.stk = (w.stk & ~(0xFFull << (8 * lv))) | ((uint64_t)w.pm << (8 * lv));
     else w.stk8 = w.pm;
     w.path |= oi << (3 * lv);
@@ -971,7 +972,7 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
 // Slots = the slot walk (walk_node_slots, RT_WALK_TIGHT) or the node_kids walk (walk_node); both give
 // the reference's result. (The wavefront's persistent walk kernels use the node_kids walk: the slot
 // walk inlined there trips an AMDGPU backend error, "illegal VGPR to SGPR copy", in ROCm 7.2.)
-template <bool Slots = (RT_WALK_TIGHT != 0)>
+template <bool Slots = (RT_WALK_TIGHT != 0), int AS = 256>
 RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w, double* t,
                      int* prim, LdsAncI32* anc = nullptr) {
     RT_DBG(5);
@@ -981,7 +982,7 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         // next triangles are tested. Leaves are still tested in visiting order and the first leaf with
         // a hit ends the walk (a leaf the node walk found beyond it is dropped): the same result, in
         // fewer steps, with both parts of a step busy in most lanes.
-        if (!w.ndone && w.nlf >= w.nle && walk_node_slots(sc, m, ray, inv, w, anc) == WALK_MISS) w.ndone = 1;
+        if (!w.ndone && w.nlf >= w.nle && walk_node_slots<AS>(sc, m, ray, inv, w, anc) == WALK_MISS) w.ndone = 1;
         RT_DBG_TSTART(t_lt);
         if (w.lpos < w.lend) {
             const int st = leaf_tris(sc, ray, w, t, prim);

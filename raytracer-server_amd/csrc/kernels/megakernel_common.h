@@ -177,13 +177,13 @@ __device__ __forceinline__ int32_t queue_take_each(const LdsQueue& q, bool want)
     return want && rank < k ? queue_read(q, h + rank) : -1;
 }
 
-// Resident grid of a persistent kernel: as many 256-thread blocks as fit on the device at once.
+// Resident grid of a persistent kernel: as many blocks (of `threads`) as fit on the device at once.
 template <class K>
-static inline long resident_blocks(K kernel, long want) {
+static inline long resident_blocks(K kernel, long want, int threads = 256) {
     int dev = 0, ncu = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu < 1) per_cu = 1;
     return std::max(1L, std::min((long)ncu * per_cu, want));
 }
 

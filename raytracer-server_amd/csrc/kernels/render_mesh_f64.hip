@@ -68,12 +68,21 @@ enum : int { PH_TRACE = 0, PH_WALK_CLOSEST = 1, PH_WALK_SHADOW = 2 };
 // Doubles: ray o, d; 1/d; box mn, mx; walk best t; query t (closest hit so far / shadow distance);
 // pending NEE term. Ints: walk cursor fields, closest hit object/prim, gen slot, mesh, occluded.
 constexpr int kParkD = 21, kParkI = 18, kParkThreads = 256;
-struct Park {  // typed in the LDS address space: ds_read/ds_write with one 32-bit base + immediate offsets
-    LdsDouble* d;  // this thread's column of [kParkD][kParkThreads]
-    LdsInt* i;     // [kParkI][kParkThreads]
-    RT_DEV LdsDouble& D(int f) const { return d[f * kParkThreads]; }
-    RT_DEV LdsInt& I(int f) const { return i[f * kParkThreads]; }
+// Threads of a walk-pool block (RT_POOL_BLOCK: 256, or 512 = one block per CU whose 8 waves share one
+// walk queue)
+#ifndef RT_POOL_BLOCK
+#define RT_POOL_BLOCK 256
+#endif
+constexpr int kPoolThreads = RT_POOL_BLOCK;
+template <int T = kParkThreads>
+struct ParkT {  // typed in the LDS address space: ds_read/ds_write with one 32-bit base + immediate offsets
+    LdsDouble* d;  // this thread's column of [kParkD][T]
+    LdsInt* i;     // [kParkI][T]
+    RT_DEV LdsDouble& D(int f) const { return d[f * T]; }
+    RT_DEV LdsInt& I(int f) const { return i[f * T]; }
 };
+using Park = ParkT<kParkThreads>;    // the per-lane walks (P = 0)
+using Park2 = ParkT<kPoolThreads>;  // the walk pool's compact park
 struct WalkRegs {  // the walk phase's working copy
     Ray wr;
     RayInv wi;
@@ -279,11 +288,11 @@ RT_DEV bool walk_round(const DevScene& sc, const Park& pk, const bool wk, const 
 // results to their owners (status word) and puts unfinished queries back. Walk steps then run with
 // the block's queries packed into full waves instead of the ~27 walking lanes of the wave that owns
 // them (the deep octree's walks are 0-40 steps long and needed by ~20% of the vertices, DESIGN.md
-// §5). The queue holds each query at most once and a block has at most 256 queries (one per path),
-// so a 256-entry ring cannot overflow.
+// §5). The queue holds each query at most once and a block has at most one query per path (thread),
+// so a ring with an entry per thread cannot overflow.
 struct WalkPool {
     LdsQueue q;
-    uint8_t* status;    // LDS [256] per owner column: 0 closest query, 1 shadow query, 2 done
+    uint8_t* status;    // LDS [block] per owner column: 0 closest query, 1 shadow query, 2 done
 };
 enum : uint8_t { POOL_CLOSEST = 0, POOL_SHADOW = 1, POOL_DONE = 2 };
 #ifndef RT_POOL_REFILL
@@ -305,7 +314,7 @@ constexpr int kPoolRefill = RT_POOL_REFILL;  // refill only when at least this m
 #endif
 constexpr int kPark2D = RT_PARK_INV ? 17 : 14, kPark2I = 17;
 enum : int { P2_T = 13, P2_HOBJ = 9, P2_HPRIM = 10, P2_OCC = 13, P2_NEAR = 16 };
-RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
+RT_DEV void park2_store(const Park2& p, const WalkRegs& r) {
     p.D(0) = r.wr.o.x; p.D(1) = r.wr.o.y; p.D(2) = r.wr.o.z;
     p.D(3) = r.wr.d.x; p.D(4) = r.wr.d.y; p.D(5) = r.wr.d.z;
     for (int k = 0; k < 3; ++k) { p.D(6 + k) = r.w.mn[k]; p.D(9 + k) = r.w.mx[k]; }
@@ -322,7 +331,7 @@ RT_DEV void park2_store(const Park& p, const WalkRegs& r) {
     p.I(9) = r.hobj; p.I(10) = r.hprim; p.I(11) = r.g; p.I(12) = r.mi; p.I(13) = r.occluded;
     p.I(14) = r.w.nlf; p.I(15) = r.w.nle;
 }
-RT_DEV void park2_load(const Park& p, WalkRegs& r) {
+RT_DEV void park2_load(const Park2& p, WalkRegs& r) {
     r.wr.o = v3(p.D(0), p.D(1), p.D(2));
     r.wr.d = v3(p.D(3), p.D(4), p.D(5));
 #if RT_PARK_INV
@@ -344,7 +353,7 @@ RT_DEV void park2_load(const Park& p, WalkRegs& r) {
     r.w.nlf = p.I(14); r.w.nle = p.I(15);
 }
 // A new pool query (see park_query); near: the meshes near the ray (mesh_near_mask).
-RT_DEV void park2_query(const Park& p, const Ray& r, const RayInv& wi, double wt, int32_t hobj, int32_t hprim,
+RT_DEV void park2_query(const Park2& p, const Ray& r, const RayInv& wi, double wt, int32_t hobj, int32_t hprim,
                         uint32_t near) {
     p.I(P2_NEAR) = (int32_t)near;
 #if RT_PARK_INV
@@ -373,7 +382,7 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
     }
     WalkRegs r;
     bool closest = false;
-    auto col = [&](int32_t c) { return Park{park_d + c, park_i + c}; };
+    auto col = [&](int32_t c) { return Park2{park_d + c, park_i + c}; };
     if (q >= 0) {
         park2_load(col(q), r);
         const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -396,8 +405,8 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
             if (!fin && r.w.cur >= 0) {
                 double t;
                 int prim;
-                const int st = walk_step<S>(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim,
-                                            S ? (LdsAncI32*)park_i + kPark2I * kParkThreads + q : nullptr);
+                const int st = walk_step<S, kPoolThreads>(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim,
+                                            S ? (LdsAncI32*)park_i + kPark2I * kPoolThreads + q : nullptr);
                 if (st != WALK_RUN) {
                     if (closest) {
                         if (st == WALK_HIT) {
@@ -416,7 +425,7 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
                 }
             }
             if (fin) {  // results for the owner's vertex phase, then the status word
-                const Park pq = col(q);
+                const Park2 pq = col(q);
                 pq.D(P2_T) = r.wt;
                 pq.I(P2_HOBJ) = r.hobj;
                 pq.I(P2_HPRIM) = r.hprim;
@@ -443,8 +452,8 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
     return true;
 }
 
-template <int F, int W, int P, bool S>
-__global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
+template <int F, int W, int P, bool S, int B = P ? kPoolThreads : 256>
+__global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
                                                                uint32_t* next_sub, long nsub, int ksteps, int wmin,
                                                                int refill, int pool_min, int pool_vmin) {
     using C = Cfg<F>;
@@ -462,16 +471,16 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
         sc.objects = s_objs;
     }
 #endif
-    __shared__ double s_park_d[(P ? kPark2D : kParkD) * kParkThreads];
+    __shared__ double s_park_d[(P ? kPark2D : kParkD) * B];
     // pool: + the slot walk's ancestor ids (walk_node_slots)
-    __shared__ int32_t s_park_i[(P ? kPark2I + (S ? kSlotAncLevels : 0) : kParkI) * kParkThreads];
-    const Park park{(LdsDouble*)s_park_d + threadIdx.x, (LdsInt*)s_park_i + threadIdx.x};
+    __shared__ int32_t s_park_i[(P ? kPark2I + (S ? kSlotAncLevels : 0) : kParkI) * B];
+    const ParkT<B> park{(LdsDouble*)s_park_d + threadIdx.x, (LdsInt*)s_park_i + threadIdx.x};
     // P = 1: one walk queue
-    __shared__ int32_t s_ring[1][P ? 256 : 1];
-    __shared__ uint8_t s_status[P ? 256 : 1];
+    __shared__ int32_t s_ring[1][P ? B : 1];
+    __shared__ uint8_t s_status[P ? B : 1];
     __shared__ uint32_t s_qhead[2], s_qtail[2];
     WalkPool wp;
-    wp.q = LdsQueue{s_ring[0], s_qhead, s_qtail, 255u};
+    wp.q = LdsQueue{s_ring[0], s_qhead, s_qtail, (uint32_t)B - 1u};
     wp.status = s_status;
     if constexpr (P) {
         s_ring[0][threadIdx.x] = -1;
@@ -481,8 +490,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     // subpixel accumulator and camera-sample buffer in LDS, as in k_megakernel_f64 (pool mode: the
     // buffer's 10 KB fit beside the park at 2 blocks per CU without the parked 1/d, RT_PARK_INV = 0)
     constexpr bool kCamBuf = !P || RT_POOL_CAMBUF;
-    __shared__ double s_acc[3 * 256], s_nbd[kCamBuf ? 3 * 256 : 1];
-    __shared__ uint64_t s_nbr[kCamBuf ? 2 * 256 : 1];
+    __shared__ double s_acc[3 * B], s_nbd[kCamBuf ? 3 * B : 1];
+    __shared__ uint64_t s_nbr[kCamBuf ? 2 * B : 1];
     LdsDouble* acc_l = (LdsDouble*)s_acc + threadIdx.x;
     LdsDouble* nbd = (LdsDouble*)s_nbd + (kCamBuf ? threadIdx.x : 0);
     LdsU64* nbr = (LdsU64*)s_nbr + (kCamBuf ? threadIdx.x : 0);
@@ -496,7 +505,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
     const long t0 = wave_ticket(next_sub, true);
     unit_of(a, t0, id, end, s);
     bool active = t0 < nunits;
-    acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
+    acc_l[0] = 0.0; acc_l[B] = 0.0; acc_l[2 * B] = 0.0;
     PathState ps;
     bool fresh = true;
     bool nvalid = false;
@@ -566,9 +575,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
             if (sample_end) {
                 fresh = true;
                 if (id < a.n_whole) {
-                    V3 acc = v3(acc_l[0], acc_l[256], acc_l[512]);
+                    V3 acc = v3(acc_l[0], acc_l[B], acc_l[2 * B]);
                     acc = acc + ps.L * a.inv_n;  // server.rs:357-358
-                    acc_l[0] = acc.x; acc_l[256] = acc.y; acc_l[512] = acc.z;
+                    acc_l[0] = acc.x; acc_l[B] = acc.y; acc_l[2 * B] = acc.z;
                     if (++s == a.n_samples) {
                         double* o = sub_buf + (size_t)id * 3;
                         o[0] = acc.x;
@@ -576,7 +585,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                         o[2] = acc.z;
                         if (++id < end) {  // the next subpixel of the run, no ticket
                             s = 0;
-                            acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
+                            acc_l[0] = 0.0; acc_l[B] = 0.0; acc_l[2 * B] = 0.0;
                             nvalid = false;
                         } else {
                             done = true;
@@ -594,7 +603,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
             // the next ray, unless a shadow query is pending or the unit is done (a new ticket first)
             if (!walking && !done) {
                 if (fresh) {
-                    if (kCamBuf && nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[256], nbd[512]), nbr[0], nbr[256]}, ps);
+                    if (kCamBuf && nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[B], nbd[2 * B]), nbr[0], nbr[B]}, ps);
                     else begin_sample(sc, a, subpixel_of(a, id), s, ps);
                     nvalid = false;
                     fresh = false;
@@ -635,7 +644,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
             }
             if (trace_now) {
                 if (fresh) {
-                    if (!P && nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[256], nbd[512]), nbr[0], nbr[256]}, ps);
+                    if (!P && nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[B], nbd[2 * B]), nbr[0], nbr[B]}, ps);
                     else begin_sample(sc, a, subpixel_of(a, id), s, ps);
                     nvalid = false;
                     fresh = false;
@@ -684,9 +693,9 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
             if (sample_end) {
                 fresh = true;
                 if (id < a.n_whole) {
-                    V3 acc = v3(acc_l[0], acc_l[256], acc_l[512]);
+                    V3 acc = v3(acc_l[0], acc_l[B], acc_l[2 * B]);
                     acc = acc + ps.L * a.inv_n;  // server.rs:357-358
-                    acc_l[0] = acc.x; acc_l[256] = acc.y; acc_l[512] = acc.z;
+                    acc_l[0] = acc.x; acc_l[B] = acc.y; acc_l[2 * B] = acc.z;
                     if (++s == a.n_samples) {
                         double* o = sub_buf + (size_t)id * 3;
                         o[0] = acc.x;
@@ -694,7 +703,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
                         o[2] = acc.z;
                         if (++id < end) {  // the next subpixel of the run, no ticket
                             s = 0;
-                            acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
+                            acc_l[0] = 0.0; acc_l[B] = 0.0; acc_l[2 * B] = 0.0;
                             nvalid = false;
                         } else {
                             done = true;
@@ -720,8 +729,8 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
         if (refill > 0 && __popcll(__ballot(need)) >= refill) {
             if (need) {
                 const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), s + 1);
-                nbd[0] = nb.d.x; nbd[256] = nb.d.y; nbd[512] = nb.d.z;
-                nbr[0] = nb.r0; nbr[256] = nb.r1;
+                nbd[0] = nb.d.x; nbd[B] = nb.d.y; nbd[2 * B] = nb.d.z;
+                nbr[0] = nb.r0; nbr[B] = nb.r1;
                 nvalid = true;
             }
         }
@@ -732,7 +741,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_mesh_f64(DevScene sc_g, R
         if (done) {
             unit_of(a, nt, id, end, s);
             active = !stop && nt < nunits;
-            acc_l[0] = 0.0; acc_l[256] = 0.0; acc_l[512] = 0.0;
+            acc_l[0] = 0.0; acc_l[B] = 0.0; acc_l[2 * B] = 0.0;
             fresh = true;
             nvalid = false;
         }
@@ -747,10 +756,11 @@ template <int F, int W, int P, bool S = (RT_WALK_TIGHT != 0)>
 static void launch_mm(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub, long nsub,
                       int ksteps, int wmin, int refill, int pool_min, int pool_vmin, double* tail_buf, size_t tail_cap,
                       hipStream_t st) {
-    const long blocks = resident_blocks(k_megakernel_mesh_f64<F, W, P, S>, (nsub + 255) / 256);
+    constexpr int B = P ? kPoolThreads : 256;
+    const long blocks = resident_blocks(k_megakernel_mesh_f64<F, W, P, S>, (nsub + B - 1) / B, B);
     RenderArgs a = a_in;
-    plan_tail(a, nsub, blocks * 256, tail_buf, tail_cap);
-    hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W, P, S>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf,
+    plan_tail(a, nsub, blocks * B, tail_buf, tail_cap);
+    hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W, P, S>), dim3((unsigned)blocks), dim3(B), 0, st, sc, a, sub_buf,
                        next_sub, nsub, ksteps, wmin, refill, pool_min, pool_vmin);
     launch_tail_sum_f64(a, sub_buf, nsub - a.n_whole, st);
 }
