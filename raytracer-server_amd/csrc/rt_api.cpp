@@ -259,6 +259,7 @@ int pack_scene(rt_scene* s) {
     // walk for every scene); the encoding itself holds ids below kSlotMaxNode
     int32_t slot_max = rt::kSlotMaxNode;
     if (const char* v = std::getenv("RT_SLOT_MAX_NODE")) slot_max = std::max(0, std::min(slot_max, std::atoi(v)));
+    if (slot_max == 0) slots_ok = false;
     for (const Mesh& m : sc.meshes) {
         rt::DevMesh dm{};
         dm.node_base = (int32_t)p.up.size();
