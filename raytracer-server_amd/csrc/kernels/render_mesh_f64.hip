@@ -68,10 +68,11 @@ enum : int { PH_TRACE = 0, PH_WALK_CLOSEST = 1, PH_WALK_SHADOW = 2 };
 // Doubles: ray o, d; 1/d; box mn, mx; walk best t; query t (closest hit so far / shadow distance);
 // pending NEE term. Ints: walk cursor fields, closest hit object/prim, gen slot, mesh, occluded.
 constexpr int kParkD = 21, kParkI = 18, kParkThreads = 256;
-// Threads of a walk-pool block (RT_POOL_BLOCK: 256, or 512 = one block per CU whose 8 waves share one
-// walk queue)
+// Threads of a walk-pool block: 512 = one block per CU (150 KB of LDS) whose 8 waves share one walk queue,
+// so a wave's pool round finds full sets of queries sooner (unicorn 1920x1080x32: 222.6 vs 219.3 Msamples/s
+// with two 256-thread blocks per CU, profiles/r04_ab.log)
 #ifndef RT_POOL_BLOCK
-#define RT_POOL_BLOCK 256
+#define RT_POOL_BLOCK 512
 #endif
 constexpr int kPoolThreads = RT_POOL_BLOCK;
 template <int T = kParkThreads>

@@ -17,6 +17,7 @@
 #                    (GRBM_GUI_ACTIVE) and the SQ instruction mix, each pass a run of its own
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (":" separates args), e.g. py:tools/configs_bench.py:--quick
 #   env:VAR=VAL[,VAR=VAL]  export for the following tasks (A/B of the RT_* switches)
+#   avail            rocprofv3 --list-avail -> $OUT/avail.txt
 #   dbgbuild         build the diagnostic library lib/variants/dbg.so (better: build it here and ship it)
 # Env: TAG (output subdirectory, default "run"), BENCH_ARGS (extra bench.py arguments).
 export TMPDIR=/tmp
@@ -99,6 +100,10 @@ for task in "$@"; do
         pmc_pass "${key}_sq2" $SQ2 -- "${P[@]}"
         pmc_pass "${key}_sq3" $SQ3 -- "${P[@]}"
         echo "pmc $key ok" ;;
+    avail)
+        # the counters rocprofv3 can collect on this device
+        timeout -k 10 120 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 || fail avail "$OUT/avail.txt"
+        grep -c . "$OUT/avail.txt" ;;
     dbgbuild)
         # diagnostic library (RT_DEBUG_COUNTERS + RT_DEBUG_TIMERS) at raytracer-server_amd/lib/variants/dbg.so
         make -s -j16 -C raytracer-server_amd BUILD=build_dbg LIB=lib/variants/dbg.so \
