@@ -459,6 +459,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
                                                                int refill, int pool_min, int pool_vmin) {
     using C = Cfg<F>;
     static_assert(C::mesh && C::compact, "mesh megakernel needs the compact tables");
+    static_assert(B % 64 == 0 && B <= 512, "whole waves, at most 8 (path_f64.h: the diagnostic builds' per-wave LDS)");
     // object table in LDS, as in k_megakernel_f64 (2 blocks per CU: 2 x 78 KB of LDS)
     DevScene sc = sc_g;
 #if RT_OPT_LDSOBJ
