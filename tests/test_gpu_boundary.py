@@ -210,4 +210,7 @@ def test_concurrent_cancellable_renders_share_one_flag(rt, gpu_scenes):
         t.join()
     dt = time.time() - t0
     timer.cancel()
-    assert out[0][2]["cancelled"] and out[1][2]["cancelled"] and dt < 3.0, (out[0][2]["cancelled"], out[1][2]["cancelled"], dt)
+    # two frames together would take ~18 s; the bound leaves room for a fresh box's first 1.7 GB workspace
+    # allocations (the split-tail scratch of each render) without accepting a missed cancel
+    assert out[0][2]["cancelled"] and out[1][2]["cancelled"] and dt < 6.0, \
+        (out[0][2]["cancelled"], out[1][2]["cancelled"], dt, out[0][2]["device_ms"], out[1][2]["device_ms"])
