@@ -15,6 +15,8 @@
 #   pmc:SCENE:W:H:SPP[:mis]   counter passes on one megakernel render (tools/prof_render.py):
 #                    HBM traffic (FETCH_SIZE / WRITE_SIZE), L2 hit rate (TCC_HIT / TCC_MISS), clock
 #                    (GRBM_GUI_ACTIVE) and the SQ instruction mix, each pass a run of its own
+#   pmcw:SCENE:W:H:SPP[:mis]  the wait / latency breakdown of one render (SQ_WAIT_*, SQ_ACTIVE_INST_*,
+#                    SQ_INST_LEVEL_* over SQ_INSTS_*: mean in-flight latency per memory class)
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (":" separates args), e.g. py:tools/configs_bench.py:--quick
 #   env:VAR=VAL[,VAR=VAL]  export for the following tasks (A/B of the RT_* switches)
 #   avail            rocprofv3 --list-avail -> $OUT/avail.txt
@@ -30,6 +32,9 @@ fail() { echo "FAIL: $1"; [ -f "$2" ] && tail -30 "$2"; exit 1; }
 # SQ passes: at most 8 SQ counters each
 SQ1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU"
 SQ2="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64"
+# wait / latency breakdown (pmcw): where waves spend the cycles they do not issue
+SQW1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM"
+SQW2="SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_INST_LEVEL_SMEM SQ_INSTS_SMEM SQ_INST_LEVEL_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY"
 SQ3="SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_LDS"
 
 pmc_pass() {  # name counters... -- command
@@ -104,6 +109,15 @@ for task in "$@"; do
         # the counters rocprofv3 can collect on this device
         timeout -k 10 120 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 || fail avail "$OUT/avail.txt"
         grep -c . "$OUT/avail.txt" ;;
+    pmcw)
+        # the wait breakdown of one megakernel render (two SQ passes, tools/pmc_report.py --waits)
+        scene=${A[1]}; w=${A[2]}; h=${A[3]}; spp=${A[4]}; extra=${A[5]}
+        P=(python tools/prof_render.py "$scene" "$w" "$h" "$spp" mk $extra)
+        key="${scene}_${w}x${h}x${spp}${extra:+_$extra}"
+        timeout -k 10 120 "${P[@]}" > "$OUT/${key}_plain.log" 2>&1 || fail "plain $key" "$OUT/${key}_plain.log"
+        pmc_pass "${key}_w1" $SQW1 -- "${P[@]}"
+        pmc_pass "${key}_w2" $SQW2 -- "${P[@]}"
+        echo "pmcw $key ok" ;;
     dbgbuild)
         # diagnostic library (RT_DEBUG_COUNTERS + RT_DEBUG_TIMERS) at raytracer-server_amd/lib/variants/dbg.so
         make -s -j16 -C raytracer-server_amd BUILD=build_dbg LIB=lib/variants/dbg.so \

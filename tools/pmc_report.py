@@ -97,6 +97,24 @@ def report(d, key, kernel):
                                "other": other / vertices},
                 "fp64_flops_per_vertex": flops / vertices, "lane_utilisation": lanes, "clock_GHz": clk,
                 "source": f"SQ PMC passes of tools/gpu_task.sh pmc:{key} (tools/pmc_report.py)"}
+    if "SQ_WAIT_INST_LDS" in c and "SQ_WAVE_CYCLES" in c:
+        wc = c["SQ_WAVE_CYCLES"]
+        out["waits"] = {  # fractions of the waves' resident cycles (pmcw passes)
+            "wait_any": c["SQ_WAIT_ANY"] / wc, "wait_inst_any": c["SQ_WAIT_INST_ANY"] / wc,
+            "wait_inst_lds": c["SQ_WAIT_INST_LDS"] / wc,
+            "active_valu": c["SQ_ACTIVE_INST_VALU"] / wc, "active_salu": c["SQ_ACTIVE_INST_SCA"] / wc,
+            "active_lds": c["SQ_ACTIVE_INST_LDS"] / wc, "active_vmem": c["SQ_ACTIVE_INST_VMEM"] / wc,
+            "source": "SQ_WAIT_ANY: waiting on a dependency (s_waitcnt: vmem / lgkm); SQ_WAIT_INST_ANY: a ready "
+                      "instruction waiting to issue; SQ_WAIT_INST_LDS: an LDS instruction waiting to issue"}
+    if "SQ_INST_LEVEL_VMEM" in c and "SQ_INSTS_VMEM" in c:
+        lat = {}
+        for k in ("VMEM", "SMEM", "LDS"):
+            if c.get(f"SQ_INSTS_{k}"):
+                lat[k.lower()] = c[f"SQ_INST_LEVEL_{k}"] / c[f"SQ_INSTS_{k}"]
+        out["mean_latency"] = dict(lat, unit="SQ_INST_LEVEL_x / SQ_INSTS_x: mean in-flight time per instruction "
+                                              "(the counters' cycle units)",
+                                   lds_bank_conflict_per_lds_inst=c.get("SQ_LDS_BANK_CONFLICT", 0) / max(1.0, c.get("SQ_INSTS_LDS", 1.0)),
+                                   active_any=c.get("SQ_ACTIVE_INST_ANY"))
     return out
 
 
