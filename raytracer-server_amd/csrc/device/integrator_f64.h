@@ -117,6 +117,26 @@ struct ShadowDefer {
     RayInv inv;       // make_inv(d), for the deferred query
 };
 
+// Where a deferred shadow query's ray goes (ShadowDefer): NoSink returns it in the ShadowDefer (o, d,
+// dist, inv); a column sink writes o, d and dist straight into the owner's LDS query columns the moment
+// shade_vertex finds the query pending, so the six doubles are not held in registers through the rest
+// of the vertex (the query-pool kernel: its only VGPR spill). The caller must own the columns then (no
+// query of this lane outstanding: the kernel shades only lanes whose s_pend reads 0).
+struct NoSink {
+    static constexpr bool lds = false;
+    RT_DEV void put(const V3&, const V3&, double) const {}
+};
+struct LdsQuerySink {
+    static constexpr bool lds = true;
+    __attribute__((address_space(3))) double* o;  // this lane's origin column: [3][stride]
+    __attribute__((address_space(3))) double* d;  // direction + distance: [4][stride]
+    int stride;
+    RT_DEV void put(const V3& org, const V3& dir, double dist) const {
+        o[0] = org.x; o[stride] = org.y; o[2 * stride] = org.z;
+        d[0] = dir.x; d[stride] = dir.y; d[2 * stride] = dir.z; d[3 * stride] = dist;
+    }
+};
+
 // Where a path keeps the two values only a mirror bounce hands on to the next vertex (read there only
 // when ps.kind == K_SPEC): `o`, the direction the reference passes on unchanged (scene.rs:178), and
 // the throughput before the bounce (Le(x') weight). RegCold: PathState's registers. LdsCold: a column
@@ -139,9 +159,10 @@ struct LdsCold {
 // Shades the hit `hr` of ps.ray. Returns true when the path continues (ps.ray is the next ray to
 // trace), false when this sample's radiance ps.L is final. The shadow ray of next-event estimation
 // is traced inline.
-template <class C, class Cold = RegCold>
+template <class C, class Cold = RegCold, class Sink = NoSink>
 RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
-                         const HitRec& hr, ShadowDefer* defer = nullptr, const Cold& cold = Cold()) {
+                         const HitRec& hr, ShadowDefer* defer = nullptr, const Cold& cold = Cold(),
+                         const Sink& sink = Sink()) {
     if (hr.obj < 0) return false;  // no hit: R = 0 (scene.rs:157, :175, :233)
     RT_DBG_REGION(6);
     const DevObject& obj = sc.objects[hr.obj];
@@ -227,10 +248,14 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
                     if (near) {
                         defer->pending = true;
                         defer->meshes = near;
-                        defer->inv = inv;
-                        defer->o = sr.o;
-                        defer->d = sr.d;
-                        defer->dist = dist;
+                        if constexpr (Sink::lds) {
+                            sink.put(sr.o, sr.d, dist);
+                        } else {
+                            defer->inv = inv;
+                            defer->o = sr.o;
+                            defer->d = sr.d;
+                            defer->dist = dist;
+                        }
                     }
                 } else {
                     vis = visible_ray<C>(sc, y, sr, dist) ? 1. : 0.;

@@ -505,6 +505,9 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
 // in fuller chunks, and no wave waits at a barrier for another wave's chunk (the block-synchronous
 // kernel spent 24% of its wave time in barrier waits, 2 waves of 4 working in phase P).
 constexpr int kFpRing = 512;  // per mesh: at most 256 closest-hit + 256 shadow queries queued at once
+#ifndef RT_FPOOL_SINK
+#define RT_FPOOL_SINK 1  // A/B: shade_vertex writes the shadow query's ray into the LDS columns (LdsQuerySink)
+#endif
 
 template <int F, int W>
 __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
@@ -622,8 +625,10 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
         const bool ready = active && __hip_atomic_load(&s_pend[tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
         RT_DBG_WAVE(9, ready);
         bool finish = false, shadow_q = false;
+#if !RT_FPOOL_SINK
         Ray sr{v3(0, 0, 0), v3(0, 0, 1)};
         double dist = 0.0;
+#endif
         uint32_t near_s = 0;
         if (ready) {
             if (spend) {  // the last vertex's NEE term, unless a mesh blocks its shadow ray (mutually_visible)
@@ -649,13 +654,21 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                 nverts += h.obj >= 0;
                 ShadowDefer df;
                 df.pending = false;
+#if RT_FPOOL_SINK
+                // the shadow query's ray goes straight into this lane's query columns (its s_pend read 0)
+                const LdsQuerySink qsink{(LdsD*)s_qo + tid, (LdsD*)s_qds + tid, kBlk};
+                const bool cont = shade_vertex<C, Cold, LdsQuerySink>(sc, a, ps, h, &df, cold, qsink);
+#else
                 const bool cont = shade_vertex<C, Cold>(sc, a, ps, h, &df, cold);
+#endif
                 traced = false;
                 if (df.pending) {  // the analytic objects let the shadow ray through; a mesh may block it
                     shadow_q = true;
                     pc = df.c;
+#if !RT_FPOOL_SINK
                     dist = df.dist;
                     sr = Ray{df.o, df.d};
+#endif
                     near_s = df.meshes;
                 }
                 if (!cont) {
@@ -671,9 +684,11 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
         if (shadow_q) {
             want_s = near_s;  // shade_vertex's mesh_near_mask of the segment (non-zero: df.pending)
             if (want_s) {
+#if !RT_FPOOL_SINK
                 s_qo[tid] = sr.o.x; s_qo[kBlk + tid] = sr.o.y; s_qo[2 * kBlk + tid] = sr.o.z;
                 s_qds[tid] = sr.d.x; s_qds[kBlk + tid] = sr.d.y; s_qds[2 * kBlk + tid] = sr.d.z;
                 s_qds[3 * kBlk + tid] = dist;
+#endif
                 spend = true;
                 smask = want_s;
             } else {  // no mesh near the shadow segment: unblocked now
