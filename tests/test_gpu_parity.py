@@ -522,3 +522,78 @@ def test_octree_first_hit_subtree_known_answer(rt, oracle, tmp_path):
         assert list(id_g) == [0, 0] and np.allclose(t_g, want, rtol=1e-12, atol=0)
         assert abs(p_g[0, 0] - x0) < 1e-4
         assert np.array_equal(t_g, t_o) and np.array_equal(p_g, p_o) and np.array_equal(n_g, n_o)
+
+
+SKINNY_SCENE = """
+[camera]
+pos = [50.0, 50.0, 300.0]
+dir = [0.0, 0.0, -1.0]
+[[objects]]
+brdf = {{ type = "diffuse", kd = [0.8, 0.8, 0.8] }}
+geometry = {{ type = "mesh", path = "{obj}" }}
+[[objects]]
+emitted = [50.0, 50.0, 50.0]
+brdf = {{ type = "diffuse", kd = [0.0, 0.0, 0.0] }}
+geometry = {{ type = "sphere", pos = [50.0, 5000.0, 50.0], r = 4.0 }}
+"""
+
+
+def _skinny_mesh_scene(tmp_path, n=3000, seed=7):
+    """Needle triangles (length 1..10, width 1e-7..1e-3) in random orientations around (50, 50, 50): the
+    meshes where the slot walk's subtree bounds (a triangle's vertex bounds padded by 1e-7 of the scene
+    scale) sit closest to the triangles' own rounding."""
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(40.0, 60.0, size=(n, 3))
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    v = np.cross(u, rng.normal(size=(n, 3)))
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    length = rng.uniform(1.0, 10.0, size=(n, 1))
+    width = 10.0 ** rng.uniform(-7.0, -3.0, size=(n, 1))
+    a, b, cc = c - 0.5 * length * u, c + 0.5 * length * u, c + width * v
+    verts = np.stack([a, b, cc], axis=1).reshape(-1, 3)
+    d = tmp_path / "skinny"
+    (d / "assets").mkdir(parents=True)
+    lines = [f"v {x!r} {y!r} {z!r}" for x, y, z in verts.tolist()]
+    lines += [f"f {3 * i + 1} {3 * i + 2} {3 * i + 3}" for i in range(n)]
+    (d / "assets" / "needles.obj").write_text("\n".join(lines) + "\n")
+    p = d / "s.toml"
+    p.write_text(SKINNY_SCENE.format(obj="needles.obj"))
+    return str(p), verts.reshape(n, 3, 3)
+
+
+def test_slot_walk_exact_on_grazing_rays(rt, oracle, tmp_path, monkeypatch):
+    """The slot walk's subtree-bounds culls (kid_tight_hit, path_f64.h) on adversarial rays: a mesh of
+    needle triangles, rays from far origins (1 to 1e5 scene units away) aimed at the triangles'
+    vertices and edges — where a ray grazes a subtree's padded bounds — with and without ulp-scale
+    offsets. The trace must be bit-identical to the walk without the culls (the same scene loaded
+    without slot tables, RT_SLOT_MAX_NODE=0: the reference's visiting order over node_kids) and to the
+    oracle's walk (geometry.rs:1237-1295)."""
+    path, tri = _skinny_mesh_scene(tmp_path)
+    slots = rt.Scene.from_toml(path)
+    monkeypatch.setenv("RT_SLOT_MAX_NODE", "0")
+    plain = rt.Scene.from_toml(path)
+    monkeypatch.delenv("RT_SLOT_MAX_NODE")
+    assert slots.info()["slot_tables"] == 1 and plain.info()["slot_tables"] == 0
+    assert slots.info()["parents"] > 8  # a deep octree
+    rng = np.random.default_rng(11)
+    n = 120000
+    k = rng.integers(0, tri.shape[0], n)
+    w = rng.uniform(size=(n, 1))
+    kind = rng.integers(0, 3, n)
+    tgt = np.where((kind == 0)[:, None], tri[k, rng.integers(0, 3, n)],                       # a vertex
+                   np.where((kind == 1)[:, None], (1 - w) * tri[k, 0] + w * tri[k, 1],         # the long edge
+                            (1 - w) * tri[k, 1] + w * tri[k, 2]))                             # a short edge
+    tgt = tgt * (1.0 + rng.choice([0.0, 1.0, -1.0], size=(n, 1)) * 2.0 ** -52 * rng.integers(0, 8, (n, 1)))
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    o = tgt - d * 10.0 ** rng.uniform(0.0, 5.0, size=(n, 1))
+    t_s, id_s, p_s, n_s = slots.trace_ray(o, d)
+    t_p, id_p, p_p, n_p = plain.trace_ray(o, d)
+    assert (id_s == 0).mean() > 0.2  # many rays reach a needle
+    assert np.array_equal(id_s, id_p) and np.array_equal(t_s, t_p), \
+        f"slot walk differs from the node_kids walk on {np.count_nonzero((id_s != id_p) | (t_s != t_p))} rays"
+    assert np.array_equal(p_s, p_p) and np.array_equal(n_s, n_p)
+    t_o, id_o, p_o, n_o = oracle.OracleScene(path).trace(o, d)
+    exact = (id_s == id_o) & (t_s == t_o) & np.all(p_s == p_o, axis=1) & np.all(n_s == n_o, axis=1)
+    assert exact.all(), f"{np.count_nonzero(~exact)} of {n} rays differ from the oracle"
