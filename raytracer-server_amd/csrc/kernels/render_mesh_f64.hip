@@ -547,10 +547,16 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
           // whose closest hit needed a walk traces its successor in the same iteration as its shading.
           if (vphase && active && !walking) {
             bool sample_end = false;
+#if RT_DEBUG_COUNTERS
+            bool after_s = false;  // diagnostic: a closest query right after this vertex's shadow query
+#endif
             if (phase == PH_WALK_SHADOW) {  // the shadow result (mutually_visible's mesh part)
                 if (!park.I(P2_OCC)) ps.L = ps.L + pc;
                 phase = PH_TRACE;
                 sample_end = !cont;
+#if RT_DEBUG_COUNTERS
+                after_s = cont;
+#endif
             } else if (phase == PH_WALK_CLOSEST) {  // the closest hit: shaded now
                 hh = HitRec{park.D(P2_T), park.I(P2_HOBJ), park.I(P2_HPRIM)};
                 has_hit = true;
@@ -565,6 +571,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
                 cont = shade_vertex<C>(sc, a, ps, hh, &df);
                 RT_DBG_TEND(8, t_sv);
                 if (df.pending) {  // shade_vertex found a mesh that could block the shadow ray
+                    RT_DBG(12);
                     park2_query(park, Ray{df.o, df.d}, df.inv, df.dist, -1, -1, df.meshes);
                     pc = df.c;
                     s_status[threadIdx.x] = POOL_SHADOW;
@@ -616,6 +623,10 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
                 const uint32_t near = mesh_near_mask<C>(sc, ps.ray, wi, h.obj >= 0 ? h.t : INFINITY);
                 RT_DBG_TEND(6, t_ta);
                 if (near) {
+                    RT_DBG(13);
+#if RT_DEBUG_COUNTERS
+                    if (after_s) RT_DBG(14);
+#endif
                     park2_query(park, ps.ray, wi, h.t, h.obj, h.prim, near);
                     s_status[threadIdx.x] = POOL_CLOSEST;
                     phase = PH_WALK_CLOSEST;

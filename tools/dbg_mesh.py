@@ -27,6 +27,8 @@ print(f"{scene} {w}x{h}x{spp} {' '.join(k + '=' + v for k, v in os.environ.items
       f"device {st['device_ms']:.1f} ms, vertices {st['vertices']}, vertices/wave-iteration {st['vertices'] / it:.1f}")
 print(f"  mesh calls {c[0]}, past cull {c[1] / calls:.3f}; per call: nodes {c[2] / calls:.2f} leaves {c[3] / calls:.2f} culled picks {c[6] / calls:.2f} "
       f"tris {c[4] / calls:.2f} steps {c[5] / calls:.2f}")
+if scene != "cubes":
+    print(f"  walk-pool queries: shadow {c[12]}, closest {c[13]}, closest right after the same vertex's shadow query {c[14]}")
 print(f"  wave iterations {c[8]}: vertex-phase lanes/iteration {c[9] / it:.1f}, walk steps/iteration {c[10] / it:.2f}, "
       f"walking lanes/step {c[11] / max(1, c[10]):.1f}")
 T = {0: "iteration", 1: "walk phase", 2: "vertex phase", 4: "refill + ticket", 7: "surface()", 9: "light_sample",
