@@ -60,7 +60,7 @@ RT_DEV bool next_mesh_walk_near(const DevScene& sc, const Ray& r, const RayInv& 
 // are the wavefront's deferred ones (closest: the analytic hit, then the meshes in gen order with
 // the reference's tie rule; shadow: the analytic objects let the ray through, then any mesh may
 // block it), so every path produces the same bits as k_megakernel_f64 (tested).
-enum : int { PH_TRACE = 0, PH_WALK_CLOSEST = 1, PH_WALK_SHADOW = 2, PH_WALK_PAIR = 3 };
+enum : int { PH_TRACE = 0, PH_WALK_CLOSEST = 1, PH_WALK_SHADOW = 2 };
 
 // The walk state of each lane lives in LDS between walk phases ("parked"), one column per thread
 // of the block, so the vertex phase runs with the register footprint of the analytic kernel and
@@ -293,24 +293,14 @@ RT_DEV bool walk_round(const DevScene& sc, const Park& pk, const bool wk, const 
 // so a ring with an entry per thread cannot overflow.
 struct WalkPool {
     LdsQueue q;
-    uint8_t* status;    // LDS [block] per owner column: 0 closest query, 1 shadow query, 2 done, 3 shadow query
-                        // then closest query (RT_POOL_PAIR)
+    uint8_t* status;    // LDS [block] per owner column: 0 closest query, 1 shadow query, 2 done
 };
-enum : uint8_t { POOL_CLOSEST = 0, POOL_SHADOW = 1, POOL_DONE = 2, POOL_PAIR = 3 };
+enum : uint8_t { POOL_CLOSEST = 0, POOL_SHADOW = 1, POOL_DONE = 2 };
 #ifndef RT_POOL_REFILL
 #define RT_POOL_REFILL 32
 #endif
-// Paired queries (RT_POOL_PAIR): a vertex whose shadow segment needs walks traces its continuation ray in
-// the same iteration, and when that ray needs walks too, both go to the pool as ONE job (the two rays
-// share their origin x): the taker walks the shadow query, then, in the same park column, the closest
-// query, so the path waits for one queue round trip instead of two. The owner adds the NEE term and
-// shades the continuation's hit in the iteration the job is done: the same operations in the same order.
-#ifndef RT_POOL_PAIR
-#define RT_POOL_PAIR 0
-#endif
 #ifndef RT_POOL_CAMBUF
-#define RT_POOL_CAMBUF (!RT_POOL_PAIR)  // A/B: the walk pool keeps a camera-sample buffer (refill pass) as
-                                        // k_megakernel_f64 (its 20 KB hold the paired queries' columns instead)
+#define RT_POOL_CAMBUF 1  // A/B: the walk pool keeps a camera-sample buffer (refill pass) as k_megakernel_f64
 #endif
 constexpr int kPoolRefill = RT_POOL_REFILL;  // refill only when at least this many lanes of the round are idle
 
@@ -323,12 +313,8 @@ constexpr int kPoolRefill = RT_POOL_REFILL;  // refill only when at least this m
 #define RT_PARK_INV 0  // A/B: the park keeps 1/d (1) or park2_load recomputes it (0; its 6 KB of LDS hold the
                        // pool's camera-sample buffer instead, RT_POOL_CAMBUF)
 #endif
-constexpr int kP2DBase = RT_PARK_INV ? 17 : 14;
-constexpr int kPark2D = kP2DBase + (RT_POOL_PAIR ? 4 : 0), kPark2I = 17 + (RT_POOL_PAIR ? 4 : 0);
+constexpr int kPark2D = RT_PARK_INV ? 17 : 14, kPark2I = 17;
 enum : int { P2_T = 13, P2_HOBJ = 9, P2_HPRIM = 10, P2_OCC = 13, P2_NEAR = 16 };
-// the paired closest query (RT_POOL_PAIR): direction, closest analytic hit (t, object, prim), its near-mesh
-// mask; and the shadow query's result once the job has moved on to the closest query
-enum : int { P2_DC = kP2DBase, P2_TC = kP2DBase + 3, P2_HOBJC = 17, P2_HPRIMC = 18, P2_NEARC = 19, P2_SOCC = 20 };
 RT_DEV void park2_store(const Park2& p, const WalkRegs& r) {
     p.D(0) = r.wr.o.x; p.D(1) = r.wr.o.y; p.D(2) = r.wr.o.z;
     p.D(3) = r.wr.d.x; p.D(4) = r.wr.d.y; p.D(5) = r.wr.d.z;
@@ -396,14 +382,13 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
         return false;
     }
     WalkRegs r;
-    bool closest = false, pair = false;
+    bool closest = false;
     auto col = [&](int32_t c) { return Park2{park_d + c, park_i + c}; };
     if (q >= 0) {
         park2_load(col(q), r);
         const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         closest = stq == POOL_CLOSEST;
-        pair = RT_POOL_PAIR && stq == POOL_PAIR;
-        if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW && !(RT_POOL_PAIR && stq == POOL_PAIR)) RT_QFAIL(3);
+        if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
     }
     RT_DBG_TEND(3, t_tk);
     for (int k = 0; k < ksteps; ++k) {
@@ -440,26 +425,6 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
                     fin |= r.g >= tables(sc)->last_mesh_g;  // none: the query's result is complete now
                 }
             }
-#if RT_POOL_PAIR
-            if (fin && pair) {  // the shadow query is answered: the job goes on with its closest query
-                const Park2 pq = col(q);
-                pq.I(P2_SOCC) = r.occluded;
-                pq.I(P2_NEAR) = pq.I(P2_NEARC);
-                r.wr.d = v3(pq.D(P2_DC), pq.D(P2_DC + 1), pq.D(P2_DC + 2));
-                r.wi = make_inv(r.wr.d);
-                r.wt = pq.D(P2_TC);
-                r.hobj = pq.I(P2_HOBJC);
-                r.hprim = pq.I(P2_HPRIMC);
-                r.g = -1;
-                r.occluded = 0;
-                r.w.cur = -1;
-                closest = true;
-                pair = false;
-                // this lane holds the query until it is finished or put back (queue_put: release)
-                __hip_atomic_store(&wp.status[q], (uint8_t)POOL_CLOSEST, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                fin = false;
-            }
-#endif
             if (fin) {  // results for the owner's vertex phase, then the status word
                 const Park2 pq = col(q);
                 pq.D(P2_T) = r.wt;
@@ -477,8 +442,7 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
                 park2_load(col(q), r);
                 const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 closest = stq == POOL_CLOSEST;
-                pair = RT_POOL_PAIR && stq == POOL_PAIR;
-                if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW && !(RT_POOL_PAIR && stq == POOL_PAIR)) RT_QFAIL(3);
+                if (RT_QCHECK && stq != POOL_CLOSEST && stq != POOL_SHADOW) RT_QFAIL(3);
             }
         }
     }
@@ -597,13 +561,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
                 hh = HitRec{park.D(P2_T), park.I(P2_HOBJ), park.I(P2_HPRIM)};
                 has_hit = true;
                 phase = PH_TRACE;
-            } else if (RT_POOL_PAIR && phase == PH_WALK_PAIR) {  // the shadow result, then the continuation's hit
-                if (!park.I(P2_SOCC)) ps.L = ps.L + pc;
-                hh = HitRec{park.D(P2_T), park.I(P2_HOBJ), park.I(P2_HPRIM)};
-                has_hit = true;
-                phase = PH_TRACE;
             }
-            bool s_now = false;  // a shadow query was issued by this iteration's shading
             if (has_hit) {
                 has_hit = false;
                 nverts += hh.obj >= 0;
@@ -619,7 +577,6 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
                     s_status[threadIdx.x] = POOL_SHADOW;
                     phase = PH_WALK_SHADOW;
                     walking = true;
-                    s_now = true;
                 } else {
                     sample_end = !cont;
                 }
@@ -652,10 +609,8 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
                     ++s;
                 }
             }
-            // the next ray, unless a shadow query is pending or the unit is done (a new ticket first);
-            // RT_POOL_PAIR: also the continuation of a vertex whose shadow query was just issued (its
-            // closest query, if any, rides with the shadow query)
-            if (RT_POOL_PAIR ? (!done && !has_hit && (!walking || (s_now && cont))) : (!walking && !done)) {
+            // the next ray, unless a shadow query is pending or the unit is done (a new ticket first)
+            if (!walking && !done) {
                 if (fresh) {
                     if (kCamBuf && nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[B], nbd[2 * B]), nbr[0], nbr[B]}, ps);
                     else begin_sample(sc, a, subpixel_of(a, id), s, ps);
@@ -670,24 +625,14 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
                 if (near) {
                     RT_DBG(13);
 #if RT_DEBUG_COUNTERS
-                    if (after_s || s_now) RT_DBG(14);
+                    if (after_s) RT_DBG(14);
 #endif
-                    if (RT_POOL_PAIR && s_now) {  // with the pending shadow query (same origin x) as one job
-                        park.D(P2_DC) = ps.ray.d.x; park.D(P2_DC + 1) = ps.ray.d.y; park.D(P2_DC + 2) = ps.ray.d.z;
-                        park.D(P2_TC) = h.t;
-                        park.I(P2_HOBJC) = h.obj;
-                        park.I(P2_HPRIMC) = h.prim;
-                        park.I(P2_NEARC) = (int32_t)near;
-                        s_status[threadIdx.x] = POOL_PAIR;
-                        phase = PH_WALK_PAIR;
-                    } else {
-                        park2_query(park, ps.ray, wi, h.t, h.obj, h.prim, near);
-                        s_status[threadIdx.x] = POOL_CLOSEST;
-                        phase = PH_WALK_CLOSEST;
-                        walking = true;
-                    }
+                    park2_query(park, ps.ray, wi, h.t, h.obj, h.prim, near);
+                    s_status[threadIdx.x] = POOL_CLOSEST;
+                    phase = PH_WALK_CLOSEST;
+                    walking = true;
                 } else {
-                    hh = h;  // shaded in the next iteration (or once the pending shadow query is answered)
+                    hh = h;  // shaded in the next iteration
                     has_hit = true;
                 }
             }
@@ -840,7 +785,7 @@ hipError_t launch_megakernel_mesh_f64(const DevScene& sc, const RenderArgs& a, d
                                       long nsub, int refill, int wmin, double* tail_buf, size_t tail_cap, hipStream_t st) {
     static const int ksteps = std::max(1, env_int("RT_MK_KSTEPS", 4));
     static const int pool = env_int("RT_MK_POOL", 1);
-    static const int pool_min = env_int("RT_MK_POOL_MIN", 32);
+    static const int pool_min = env_int("RT_MK_POOL_MIN", 48);  // 48 with the 512-thread pool (32 before)
     static const int pool_ksteps = std::max(1, env_int("RT_MK_POOL_KSTEPS", 6));
     static const int pool_vmin = env_int("RT_MK_POOL_VMIN", 0);
     static const int pool_refill = env_int("RT_MK_POOL_CAM_REFILL", 20);  // the walk pool's camera refill threshold

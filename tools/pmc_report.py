@@ -99,22 +99,21 @@ def report(d, key, kernel):
                 "source": f"SQ PMC passes of tools/gpu_task.sh pmc:{key} (tools/pmc_report.py)"}
     if "SQ_WAIT_INST_LDS" in c and "SQ_WAVE_CYCLES" in c:
         wc = c["SQ_WAVE_CYCLES"]
+        # SQ cycle counters tick once per 4 cycles: resident waves per SIMD = 4 WAVE_CYCLES / (SIMDs x cycles)
+        clk = out.get("clock_GHz") or 2.4
+        wps = 4 * wc / (N_SIMD * clk * dur)
         out["waits"] = {  # fractions of the waves' resident cycles (pmcw passes)
+            "waves_per_simd": wps, "clock_GHz_assumed": None if "clock_GHz" in out else clk,
             "wait_any": c["SQ_WAIT_ANY"] / wc, "wait_inst_any": c["SQ_WAIT_INST_ANY"] / wc,
             "wait_inst_lds": c["SQ_WAIT_INST_LDS"] / wc,
             "active_valu": c["SQ_ACTIVE_INST_VALU"] / wc, "active_salu": c["SQ_ACTIVE_INST_SCA"] / wc,
             "active_lds": c["SQ_ACTIVE_INST_LDS"] / wc, "active_vmem": c["SQ_ACTIVE_INST_VMEM"] / wc,
-            "source": "SQ_WAIT_ANY: waiting on a dependency (s_waitcnt: vmem / lgkm); SQ_WAIT_INST_ANY: a ready "
-                      "instruction waiting to issue; SQ_WAIT_INST_LDS: an LDS instruction waiting to issue"}
-    if "SQ_INST_LEVEL_VMEM" in c and "SQ_INSTS_VMEM" in c:
-        lat = {}
-        for k in ("VMEM", "SMEM", "LDS"):
-            if c.get(f"SQ_INSTS_{k}"):
-                lat[k.lower()] = c[f"SQ_INST_LEVEL_{k}"] / c[f"SQ_INSTS_{k}"]
-        out["mean_latency"] = dict(lat, unit="SQ_INST_LEVEL_x / SQ_INSTS_x: mean in-flight time per instruction "
-                                              "(the counters' cycle units)",
-                                   lds_bank_conflict_per_lds_inst=c.get("SQ_LDS_BANK_CONFLICT", 0) / max(1.0, c.get("SQ_INSTS_LDS", 1.0)),
-                                   active_any=c.get("SQ_ACTIVE_INST_ANY"))
+            # the SIMD's view: the share of its cycles with a VALU (SALU) instruction of some wave executing
+            "simd_valu_busy": c["SQ_ACTIVE_INST_VALU"] / wc * wps, "simd_salu_busy": c["SQ_ACTIVE_INST_SCA"] / wc * wps,
+            "lds_bank_conflict_cycles": c.get("SQ_LDS_BANK_CONFLICT", 0) / wc if "SQ_LDS_BANK_CONFLICT" in c else None,
+            "source": "SQ_WAIT_ANY: a wave waiting on a dependency (s_waitcnt: memory / LDS / scalar loads); "
+                      "SQ_WAIT_INST_ANY: a wave with a ready instruction waiting to issue (another wave holds the "
+                      "unit); SQ_ACTIVE_INST_VALU: cycles a wave's VALU instruction executes"}
     return out
 
 
