@@ -193,12 +193,21 @@ def compute_block(mix, vertices, kernel_ms):
     cyc = sum(mix["per_vertex"][c] * VALU_COST[c] for c in VALU_COST) * rate
     clock = mix["clock_GHz"] * 1e9
     flops = mix["fp64_flops_per_vertex"] * rate
-    return {"bound": "valu_issue_f64", "issue_frac": round(cyc / (N_SIMD * clock), 4),
+    out = {"bound": "valu_issue_f64", "issue_frac": round(cyc / (N_SIMD * clock), 4),
             "issue_cycles_per_s": round(cyc, 1), "clock_GHz": mix["clock_GHz"],
             "valu_inst_per_vertex": round(sum(mix["per_vertex"].values()), 2),
             "fp64_tflops": round(flops / 1e12, 3), "fp64_peak_tflops": FP64_PEAK_TFLOPS,
             "fp64_frac": round(flops / 1e12 / FP64_PEAK_TFLOPS, 4), "lane_utilisation": mix["lane_utilisation"],
             "cost_cycles": VALU_COST, "source": mix["source"]}
+    if mix.get("waits"):  # the SIMD's measured view (SQ_ACTIVE_INST_VALU, SQ_WAIT_*: pmcw passes)
+        w = mix["waits"]
+        out["simd_valu_busy"] = round(w["simd_valu_busy"], 4)
+        out["simd_salu_busy"] = round(w["simd_salu_busy"], 4)
+        out["wave_wait_dependency"] = round(w["wait_any"], 4)
+        out["wave_wait_issue"] = round(w["wait_inst_any"], 4)
+        out["waits_source"] = ("SQ_ACTIVE_INST_VALU x waves/SIMD: share of SIMD cycles with a VALU instruction "
+                               "executing; SQ_WAIT_ANY / SQ_WAIT_INST_ANY per resident wave-cycle")
+    return out
 
 
 def main():

@@ -5,8 +5,10 @@ python tools/configs_bench.py [--quick] [--fp32] [--json]
   --json  one bench-style JSON line per config instead of the text line: value, roofline (SURVEY §8(d):
           88 B per camera sample + 280 B per path vertex over the device time; for mesh scenes also the
           scene bytes touched, 32 B per parent visit + 8 B per leaf + (4 + 36) B per triangle test, from
-          the walk counters of the diagnostic build lib/variants/dbg.so run in a subprocess at 16 spp;
-          and the compute block from the scene's committed PMC summary profiles/<round>_pmc_<scene>_*.json)
+          the walk counters of the diagnostic build lib/variants/dbg.so run in a subprocess on the same workload;
+          the compute block and the measured traffic (2 x FETCH_SIZE + WRITE_SIZE) from the newest committed PMC
+          summary of exactly this workload, profiles/<round>_pmc_<scene>_<W>x<H>x<SPP>[_mis].json, else of the
+          scene at another size, scaled per sample and labelled)
           and cpu_baseline (the config's line in profiles/r03_cpu_configs.log, tools/cpu_configs.py)
 C5 is 4096x4096 at 64 of its 4096 spp on 1 GPU (stated in the line; the per-rank share at full spp is
 tools/tail_probe.py share ...)."""
@@ -47,39 +49,49 @@ s = rt_amd.Scene.from_toml(os.path.join(os.environ["RT_REPO"], "scenes", sys.arg
 c = (ctypes.c_ulonglong * 16)()
 rt_amd.render(s, 64, 48, 4, megakernel=True)
 rt_amd.lib.rt_debug_counters(c)
-_, _, st = rt_amd.render(s, int(sys.argv[2]), int(sys.argv[3]), 16, megakernel=True, mis=sys.argv[4] == "1")
+_, _, st = rt_amd.render(s, int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[5]), megakernel=True, mis=sys.argv[4] == "1")
 rt_amd.lib.rt_debug_counters(c)
 print(json.dumps({"calls": c[0], "parent_visits": c[2], "leaves": c[3], "tri_tests": c[4], "vertices": st["vertices"],
                   "samples": st["samples"]}))
 """
 
 
-def walk_counters(scene, w, h, mis):
-    """Per-vertex octree walk counters of the diagnostic build (None if it is not built)."""
+def walk_counters(scene, w, h, mis, spp):
+    """Per-vertex octree walk counters of the diagnostic build on the same workload (None if it is not built)."""
     lib = os.path.join(REPO, "raytracer-server_amd", "lib", "variants", "dbg.so")
     if not os.path.exists(lib):
         return None
     env = dict(os.environ, RT_AMD_LIB=lib, RT_REPO=REPO)
-    out = subprocess.run([sys.executable, "-c", _WALK_SCRIPT, scene, str(w), str(h), "1" if mis else "0"], env=env,
+    out = subprocess.run([sys.executable, "-c", _WALK_SCRIPT, scene, str(w), str(h), "1" if mis else "0", str(spp)], env=env,
                          capture_output=True, text=True, timeout=300)
     if out.returncode != 0:
         return None
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
-def pmc_mix(scene, mis):
-    """The newest committed PMC instruction mix of this scene's megakernel (tools/pmc_report.py)."""
+def _round_key(f):
+    """Sort key of profiles/r<NN><tag>_pmc_*.json files: newest round (then tag) last."""
+    b = os.path.basename(f)
+    return (b[1:3], b.split("_pmc_")[0], b)
+
+
+def pmc_summary(scene, w, h, spp, mis):
+    """The newest committed PMC summary (tools/pmc_report.py) of exactly this workload, else of the scene's
+    megakernel at another size: (summary, path, exact)."""
+    tag = f"{scene}_{w}x{h}x{spp}{'_mis' if mis else ''}"
+    exact = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{tag}.json")), key=_round_key)
     pat = os.path.join(REPO, "profiles", f"r*_pmc_{scene}_*{'_mis' if mis else ''}.json")
-    files = sorted(f for f in glob.glob(pat) if mis or "_mis" not in os.path.basename(f))
-    for f in reversed(files):
-        try:
-            with open(f) as fh:
-                d = json.load(fh)
+    other = sorted((f for f in glob.glob(pat) if mis or "_mis" not in os.path.basename(f)), key=_round_key)
+    for files, is_exact in ((exact, True), (other, False)):
+        for f in reversed(files):
+            try:
+                with open(f) as fh:
+                    d = json.load(fh)
+            except (OSError, ValueError):
+                continue
             if d.get("valu_mix"):
-                return d["valu_mix"], os.path.relpath(f, REPO)
-        except (OSError, ValueError):
-            continue
-    return None, None
+                return d, os.path.relpath(f, REPO), is_exact
+    return None, None, False
 
 
 def cpu_rates():
@@ -119,12 +131,16 @@ for label, name, w, h, spp, mis in CONFIGS:
                        "spp": spp, "mis": mis, "mode": "megakernel" + ("-f32" if fp32 else ""),
                        "vertices": st["vertices"], "vertices_per_sample": round(st["vertices"] / n, 4),
                        "device_ms": round(st["device_ms"], 3)},
-            "roofline": {"bound": "hbm", "achieved": round(model / sec / 1e9, 2), "peak": bench.HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(model / sec / 1e9 / bench.HBM_PEAK_GBS, 4), "traffic": None,
-                         "algorithmic_bytes_per_launch": model,
+            "roofline": {"bound": "valu_issue_f64" if not fp32 else "valu_issue_f32",
+                         "achieved": round(model / sec / 1e9, 2), "peak": bench.HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(model / sec / 1e9 / bench.HBM_PEAK_GBS, 4),
+                         "frac_meaning": "SURVEY 8(d)'s wavefront model (a model ceiling, not bytes moved)",
+                         "model_ceiling_Msamples": round(bench.HBM_PEAK_GBS * 1e9 / (bench.BYTES_PER_SAMPLE +
+                                                         bench.BYTES_PER_VERTEX * st["vertices"] / n) / 1e6, 1),
+                         "traffic": None, "algorithmic_bytes_per_launch": model,
                          "algorithmic_model": "SURVEY 8(d): 88 B per camera sample + 280 B per path vertex"}}
     if name != "cornell_box" and not fp32:
-        wc = walk_counters(name, min(w, 1920), min(h, 1080), mis)
+        wc = walk_counters(name, w, h, mis, spp)
         if wc and wc["vertices"] and wc["calls"]:  # (flat meshes, the cubes: flat_query, no walk counters)
             per_v = {k: wc[k] / wc["vertices"] for k in ("calls", "parent_visits", "leaves", "tri_tests")}
             sb_v = 32 * per_v["parent_visits"] + 8 * per_v["leaves"] + 40 * per_v["tri_tests"]
@@ -134,11 +150,26 @@ for label, name, w, h, spp, mis in CONFIGS:
                 "per_vertex": round(sb_v, 2), "GBps": round(sb_v * st["vertices"] / sec / 1e9, 2),
                 "walks_per_vertex": round(per_v["calls"], 4),
                 "per_walk": {k: round(wc[k] / max(1, wc["calls"]), 3) for k in ("parent_visits", "leaves", "tri_tests")},
-                "source": "walk counters of lib/variants/dbg.so (RT_DEBUG_COUNTERS) on the same scene at 16 spp"}
-    mix, src = pmc_mix(name, mis)
-    if mix and not fp32:
-        line["roofline"]["compute"] = bench.compute_block(mix, st["vertices"], st["device_ms"])
-        line["roofline"]["compute"]["source"] = src
+                "source": "walk counters of lib/variants/dbg.so (RT_DEBUG_COUNTERS) on this workload"}
+    pmc, src, exact = pmc_summary(name, w, h, spp, mis) if not fp32 else (None, None, False)
+    if pmc:
+        rf = line["roofline"]
+        rf["compute"] = bench.compute_block(pmc["valu_mix"], st["vertices"], st["device_ms"])
+        rf["compute"]["source"] = src
+        if pmc.get("waits"):
+            rf["compute"]["simd_valu_busy"] = round(pmc["waits"]["simd_valu_busy"], 4)
+            rf["compute"]["wait_any"] = round(pmc["waits"]["wait_any"], 4)
+        hbm = pmc.get("hbm")
+        if hbm and pmc.get("samples"):
+            # the measured HBM bytes of the launch (2 x FETCH_SIZE + WRITE_SIZE); from another size of the same
+            # scene scaled per sample (labelled)
+            traffic = hbm["bytes"] if exact else hbm["bytes"] / pmc["samples"] * n
+            rf["traffic"] = int(traffic)
+            rf["measured_frac"] = round(traffic / sec / 1e9 / bench.HBM_PEAK_GBS, 6)
+            rf["traffic_source"] = (f"{src}: 2 x FETCH_SIZE + WRITE_SIZE of this workload's launch" if exact else
+                                    f"{src}: 2 x FETCH_SIZE + WRITE_SIZE per sample of {pmc['workload']}, x {n} samples")
+            if pmc.get("l2_hit_rate") is not None:
+                rf["l2_hit_rate"] = round(pmc["l2_hit_rate"], 4)
     c = cpu.get(label.split(" (")[0]) or next((v for k, v in cpu.items() if k.startswith(label.split(" (")[0])), None)
     if c:
         line["cpu_baseline"] = {"value": c["all_cores"]["Msamples_per_s"], "unit": "Msamples/s", "cores": c["cores"],

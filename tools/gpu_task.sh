@@ -80,6 +80,8 @@ for task in "$@"; do
         pmc_pass bench_sq1 $SQ1 -- "${B[@]}"
         pmc_pass bench_sq2 $SQ2 -- "${B[@]}"
         pmc_pass bench_sq3 $SQ3 -- "${B[@]}"
+        pmc_pass bench_w1 $SQW1 -- "${B[@]}"
+        pmc_pass bench_w2 $SQW2 -- "${B[@]}"
         line=$(grep '^{"metric"' "$OUT/bench_fetch.log" | tail -1)
         key=$(echo "$line" | python -c "import json,sys;d=json.loads(sys.stdin.read());print(d['config']['workload'],d['config']['mode'])")
         # pmc_report.py reads the workload's sample / vertex counts and device time from a plain log

@@ -129,6 +129,9 @@ def main():
     d, key = args[0], args[1]
     kernel = args[2] if len(args) > 2 else "megakernel"
     r = report(d, key, kernel)
+    if "waits" in r and "valu_mix" in r:
+        r["valu_mix"]["waits"] = {k: r["waits"][k] for k in ("simd_valu_busy", "simd_salu_busy", "wait_any",
+                                                              "wait_inst_any", "waves_per_simd")}
     print(json.dumps(r, indent=1))
     if "--out" in sys.argv:
         path = sys.argv[sys.argv.index("--out") + 1]
