@@ -628,7 +628,7 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
     w.nlf = w.nle = 0;
     w.ndone = 0;
     w.enter = 0;
-    w.cur = m.node_base;
+    w.cur = Slots ? m.root_pid : m.node_base;  // the slot walk names parents by their row (pid)
     w.depth = 0;
     w.path = 0;
     w.stk = 0;

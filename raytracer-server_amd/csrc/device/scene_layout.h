@@ -52,7 +52,8 @@ struct alignas(16) DevMesh {
     double total_weight;      // sum of triangle areas (WeightedIndex total)
     double cull_pad;          // near_box padding: 1e-7 * max(1, |box coordinates|)
     int32_t btri_base;        // first of this mesh's n_tris BVH-order triangles (DevScene::btris)
-    int32_t pad5;
+    int32_t root_pid;         // the root's row in DevScene::node_slot / node_box (parent ordinal), -1 for a
+                              // root leaf
     int32_t root_exist;       // the root's existence mask (KidSlot): the slot walk's first walk_enter
     int32_t pad2;
     double tight_base[3], tight_step;  // KidSlot bounds: base[k] + q * step (cull box min - E, 3 E / 65535)
@@ -89,7 +90,7 @@ RT_LAYOUT_FN int32_t kid_leaf(int32_t leaf, int32_t first, int32_t count) {
     const bool inl = count < kKidCountEscape && first < (1 << 25);
     return -2 - ((inl ? first : leaf) << 6 | (inl ? count : kKidCountEscape));
 }
-// A walk's child pick reads one 16-byte slot: node_slot[node][8] = the child entry (as node_kids,
+// A walk's child pick reads one 16-byte slot: node_slot[pid][8] = the child entry (as node_kids,
 // with the parent encoding below) and the child subtree's triangle
 // bounds ("tight box": the vertices of every triangle in the subtree's leaves, padded by
 // DevMesh::cull_pad), rounded OUTWARD to 16-bit codes over the mesh's range (DevMesh::tight_base /
@@ -99,8 +100,11 @@ RT_LAYOUT_FN int32_t kid_leaf(int32_t leaf, int32_t first, int32_t count) {
 // padding from them cannot get tri_intersect == true from any triangle below, so the reference's walk
 // would find nothing there: skipping the child changes no result (Octree).
 // A parent child's entry in a slot also carries that child's own existence mask (bit k: its octant k
-// holds a node), so entering it needs no load: entry = node id | mask << 23 (ids < 2^23); leaf and
-// empty entries as in node_kids.
+// holds a node), so entering it needs no load: entry = pid | mask << 23 (pids < 2^23); leaf and
+// empty entries as in node_kids. The slot walk refers to parents only (leaves are inline in the
+// entries), so node_slot and node_box are indexed by the parent ordinal `pid` (parents numbered in the
+// octree's DFS order, over all meshes): 9,540 rows for the unicorn instead of one per node (47,183), and
+// a pop's box load no longer shares its cache lines with the boxes of leaves.
 struct alignas(16) KidSlot {
     int32_t kid;
     uint16_t lo[3], hi[3];
@@ -193,10 +197,10 @@ struct DevScene {
     const Bvh32* bvh32;
     const Tri32* btris32;
     const Compact32* ctab32;    // f32 compact tables (ok == 0: the generic object loop)
-    const KidSlot* node_slot;   // [node][8] child entry + subtree triangle bounds (KidSlot above); null
+    const KidSlot* node_slot;   // [pid][8] child entry + subtree triangle bounds (KidSlot above); null
                                 // when a node id does not fit a slot entry (>= kSlotMaxNode): the walks
                                 // then read node_kids (walk_step<false>)
-    const double* node_box;     // [node][6] the node's octant box (min xyz, max xyz) with the walk's own
+    const double* node_box;     // [pid][6] the parent's octant box (min xyz, max xyz) with the walk's own
                                 // arithmetic: a pop of the slot walk reloads the ancestor's box from here
     int32_t pad6, pad7;
     float off32;                // f32 mode: hit points are offset by off32 * n (scene-scaled epsilon)

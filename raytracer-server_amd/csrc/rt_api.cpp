@@ -56,9 +56,9 @@ struct Packed {
     std::vector<rt::DevBvhNode> bvh;  // nearest-triangle mode (RT_FLAG_MESH_NEAREST)
     std::vector<rt::DevTri> btris;
     std::vector<int32_t> btri_id;
-    std::vector<rt::KidSlot> slots;      // [node][8] child entry + subtree triangle bounds (scene_layout.h KidSlot);
+    std::vector<rt::KidSlot> slots;      // [pid][8] child entry + subtree triangle bounds (scene_layout.h KidSlot);
                                          // empty when a node id does not fit a slot entry (the node_kids walk)
-    std::vector<double> node_box;        // [node][6] octant boxes, the walk's arithmetic (DevScene::node_box)
+    std::vector<double> node_box;        // [pid][6] parents' octant boxes, the walk's arithmetic (DevScene::node_box)
 };
 
 // A child slot (scene_layout.h KidSlot): the child entry and its subtree's triangle bounds b (lo xyz,
@@ -247,9 +247,10 @@ void build_bvh(Packed& p, const rt::host::Mesh& m, int32_t tri_base) {
     if (n > 0) rec.build(0, n, 0);
 }
 
-// RT_OK, or RT_E_INVAL when the octree tables cannot encode the mesh (kid_leaf: leaf ids < 2^25). Node ids
-// beyond a KidSlot entry's range (>= kSlotMaxNode, global over the scene's meshes) leave the scene without
-// slot tables: its walks then read node_kids (walk_step<false>, the same result without the subtree culls).
+// RT_OK, or RT_E_INVAL when the octree tables cannot encode the mesh (kid_leaf: leaf ids < 2^25). Parent
+// ordinals beyond a KidSlot entry's range (>= kSlotMaxNode, counted over the scene's meshes) leave the scene
+// without slot tables: its walks then read node_kids (walk_step<false>, the same result without the
+// subtree culls).
 int pack_scene(rt_scene* s) {
     using namespace rt::host;
     Packed& p = s->packed;
@@ -423,15 +424,13 @@ int pack_scene(rt_scene* s) {
             }
             // every node's box as the walk computes it: the root box, then per level the octant of the
             // parent's box with c = (mn + mx) / 2 (path_f64.h walk_node_slots; DFS pre-order: parents first)
-            const size_t nb0 = p.node_box.size();
-            p.node_box.resize(nb0 + 6 * oc.size());
-            double* nb = p.node_box.data() + nb0;
+            std::vector<double> nb(6 * oc.size());
             for (size_t j = 0; j < oc.size(); ++j) {
                 if (oc.parent[j] < 0) {
-                    std::memcpy(nb + 6 * j, rbox, sizeof rbox);
+                    std::memcpy(&nb[6 * j], rbox, sizeof rbox);
                     continue;
                 }
-                const double* pb = nb + 6 * (size_t)oc.parent[j];
+                const double* pb = &nb[6 * (size_t)oc.parent[j]];
                 const uint32_t oi = (uint32_t)oc.slot[j];
                 for (int k = 0; k < 3; ++k) {
                     const double c = (pb[k] + pb[3 + k]) / 2.0;
@@ -440,6 +439,14 @@ int pack_scene(rt_scene* s) {
                     nb[6 * j + 3 + k] = hi ? pb[3 + k] : c;
                 }
             }
+            // parent ordinals (pid, the slot walk's rows: scene_layout.h KidSlot), DFS order, over all meshes
+            std::vector<int32_t> pid(oc.size(), -1);
+            for (size_t j = 0; j < oc.size(); ++j)
+                if (!oc.kind[j]) {
+                    pid[j] = (int32_t)(p.node_box.size() / 6);
+                    p.node_box.insert(p.node_box.end(), &nb[6 * j], &nb[6 * j] + 6);
+                }
+            dm.root_pid = oc.size() > 0 && !oc.kind[0] ? pid[0] : -1;
             // the 16-bit code range: the cull box's min - E .. min + 2E per axis (E its largest extent)
             double E = 0.0;
             for (int k = 0; k < 3; ++k) E = std::fmax(E, dm.cull_box[3 + k] - dm.cull_box[k]);
@@ -449,6 +456,7 @@ int pack_scene(rt_scene* s) {
             if (oc.size() > 0 && !oc.kind[0])
                 for (int q = 0; q < 8; ++q) dm.root_exist |= (oc.child[q] >= 0 ? 1 : 0) << q;
             for (size_t j = 0; j < oc.size(); ++j) {
+                if (oc.kind[j]) continue;  // rows for parents only (row pid[j])
                 for (int k = 0; k < 8; ++k) {
                     const int32_t c8 = oc.child[8 * j + k];
                     double b[6] = {0, 0, 0, 0, 0, 0};
@@ -458,8 +466,9 @@ int pack_scene(rt_scene* s) {
                             b[3 + q] = sb[6 * (size_t)c8 + 3 + q] + dm.cull_pad;
                         }
                     int32_t e = p.kids[8 * (j + (size_t)dm.node_base) + k];
-                    if (e >= slot_max) slots_ok = false;  // checked after the loop: no slot tables
-                    if (e >= 0) {  // a parent: its node id and its own existence mask (KidSlot)
+                    if (e >= 0) {  // a parent: its row (pid) and its own existence mask (KidSlot)
+                        e = pid[c8];
+                        if (e >= slot_max) slots_ok = false;  // checked after the loop: no slot tables
                         uint32_t ex = 0;
                         for (int q = 0; q < 8; ++q) ex |= (oc.child[8 * (size_t)c8 + q] >= 0 ? 1u : 0u) << q;
                         e = rt::slot_parent(e, ex);
