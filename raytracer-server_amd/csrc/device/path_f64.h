@@ -628,7 +628,9 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
     w.nlf = w.nle = 0;
     w.ndone = 0;
     w.enter = 0;
-    w.cur = Slots ? m.root_pid : m.node_base;  // the slot walk names parents by their row (pid)
+    // the slot walk names parents by their row (pid); a root leaf has none, and its walk never reads `cur`
+    // (no children to pick), but cur >= 0 is what marks a walk in progress (pool_round)
+    w.cur = Slots ? max(m.root_pid, 0) : m.node_base;
     w.depth = 0;
     w.path = 0;
     w.stk = 0;
@@ -768,7 +770,7 @@ RT_DEV int4 kid_slot(const DevScene& sc, int32_t cur, uint32_t oi) {
 // The node part of a walk step through the child slots (RT_WALK_TIGHT): as walk_node below, but a
 // pick reads the child's 16-byte slot (entry + subtree triangle bounds) and skips children whose
 // bounds the ray misses (up to two picks per step), and a descent takes the new node's existence
-// mask from the entry (no load). `anc` (or null: the node_up chain): this walk's LDS column of
+// mask from the entry (no load). `anc` (or null: the pid_up chain): this walk's LDS column of
 // ancestor node ids at depths 0 .. kSlotAncLevels - 1 (stride 256 threads), written at each descent,
 // so a pop reads the node it resumes at from LDS.
 constexpr int kSlotAncLevels = 9;
@@ -800,9 +802,9 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
         }
         if (anc) {
             w.cur = anc[lv * AS];
-        } else {
+        } else {  // the parent chain by pid (rows of node_slot / node_box)
             int32_t cur = w.cur;
-            for (int l = w.depth; l > lv; --l) cur = sc.node_up[cur].x;
+            for (int l = w.depth; l > lv; --l) cur = sc.pid_up[cur];
             w.cur = cur;
         }
         w.depth = lv;

@@ -59,6 +59,7 @@ struct Packed {
     std::vector<rt::KidSlot> slots;      // [pid][8] child entry + subtree triangle bounds (scene_layout.h KidSlot);
                                          // empty when a node id does not fit a slot entry (the node_kids walk)
     std::vector<double> node_box;        // [pid][6] parents' octant boxes, the walk's arithmetic (DevScene::node_box)
+    std::vector<int32_t> pid_up;         // [pid] the parent's parent as a pid, -1 at the root (DevScene::pid_up)
 };
 
 // A child slot (scene_layout.h KidSlot): the child entry and its subtree's triangle bounds b (lo xyz,
@@ -447,6 +448,8 @@ int pack_scene(rt_scene* s) {
                     p.node_box.insert(p.node_box.end(), &nb[6 * j], &nb[6 * j] + 6);
                 }
             dm.root_pid = oc.size() > 0 && !oc.kind[0] ? pid[0] : -1;
+            for (size_t j = 0; j < oc.size(); ++j)  // each parent's own parent, as a pid (the slot walk's pops
+                if (!oc.kind[j]) p.pid_up.push_back(oc.parent[j] >= 0 ? pid[oc.parent[j]] : -1);  // without anc)
             // the 16-bit code range: the cull box's min - E .. min + 2E per axis (E its largest extent)
             double E = 0.0;
             for (int k = 0; k < 3; ++k) E = std::fmax(E, dm.cull_box[3 + k] - dm.cull_box[k]);
@@ -479,7 +482,10 @@ int pack_scene(rt_scene* s) {
         }
         p.meshes.push_back(dm);
     }
-    if (!slots_ok) p.slots.clear();
+    if (!slots_ok) {
+        p.slots.clear();
+        p.pid_up.clear();
+    }
     for (const Object& o : sc.objects) {
         rt::DevObject d{};
         d.geom = o.geom;
@@ -688,8 +694,9 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         put(blob, &o_tri32, tri32);
         size_t o_slot;
         put(blob, &o_slot, p.slots);
-        size_t o_nbox;
+        size_t o_nbox, o_pup;
         put(blob, &o_nbox, p.node_box);
+        put(blob, &o_pup, p.pid_up);
         void* d = nullptr;
         HIP_TRY(hipMalloc(&d, blob.size()));
         hipError_t e = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice);
@@ -721,6 +728,7 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.compact = compact;
         ds.node_slot = p.slots.empty() ? nullptr : (const rt::KidSlot*)(b + o_slot);
         ds.node_box = (const double*)(b + o_nbox);
+        ds.pid_up = p.slots.empty() ? nullptr : (const int32_t*)(b + o_pup);
         ds.light = s->host.light;
         ds.light_pdf = 0.0;
         if (ds.light >= 0 && ds.light < (int32_t)p.objects.size()) {
