@@ -562,6 +562,10 @@ __shared__ unsigned long long s_dbg_time[8 * 16];
 #ifndef RT_WALK_TIGHT
 #define RT_WALK_TIGHT 1  // A/B: 0 = visit every child whose octant box the ray hits (the reference's walk)
 #endif
+#ifndef RT_WALK_HOIST
+#define RT_WALK_HOIST 0  // A/B: the slot walk loads the open leaf's triangles before its node operation (1),
+                         // or tests them first with the node operation's loads fetched ahead (2)
+#endif
 struct OctWalk {
     double mn[3], mx[3];  // box of `cur`
     int32_t cur, depth;
@@ -736,6 +740,28 @@ RT_DEV int leaf_tris(const DevScene& sc, const Ray& ray, OctWalk& w, double* t, 
     }
     return -1;
 }
+// The tests of leaf_tris on triangles already loaded (the slot walk's hoisted loads, walk_step<true>).
+RT_DEV int leaf_tris_loaded(const DevScene& sc, const Ray& ray, OctWalk& w, const DevTri* tr, double* t, int* prim) {
+#pragma unroll
+    for (int j = 0; j < kTrisPerStep; ++j) {
+        if (w.lpos < w.lend) {
+            RT_DBG(4);
+            double tt;
+            if (tri_t(tr[j], ray, &tt) && (w.best < 0 || tt < w.bt)) {
+                w.bt = tt;
+                w.best = w.lpos;
+            }
+            ++w.lpos;
+        }
+    }
+    if (w.lpos < w.lend) return WALK_RUN;
+    if (w.best >= 0) {
+        *t = w.bt;
+        *prim = sc.ltri_id[w.best];
+        return WALK_HIT;
+    }
+    return -1;
+}
 // Could any triangle below the child of slot `ks` (scene_layout.h KidSlot) return tri_intersect ==
 // true for this ray? false only if the ray (t >= 0) passes farther than the padding from the child
 // subtree's triangle bounds: the same conservative slab test as near_box. Skipping such a child leaves
@@ -780,16 +806,66 @@ constexpr int kSlotAncLevels = 9;
 #ifndef RT_SLOT_CULL
 #define RT_SLOT_CULL 1  // A/B: 0 = the slot walk without the subtree-bounds test
 #endif  // the deepest parents sit at depth 8 (MAX_DEPTH 10, root depth 1)
+// What the next node operation will load, fetched ahead (RT_WALK_HOIST=2: at the start of the step,
+// before its triangle tests): kind 1 = a pick at `cur` (its first candidate's slot), kind 2 = a pop to
+// the ancestor `cur` at level `lv` (its box and its first candidate's slot), 0 = nothing (the root still
+// to be entered, or exhausted). The node state this reads is not touched by the triangle tests, so the
+// node operation after them starts from the same state and uses these values instead of loading.
+struct SlotPF {
+    int4 ks;
+    double2 b0, b1, b2;
+    int32_t cur, lv;
+    uint32_t pm;
+    int kind;
+};
+template <int AS = 256>
+RT_DEV void slot_prefetch(const DevScene& sc, const OctWalk& w, const LdsAncI32* anc, SlotPF& pf) {
+    pf.kind = 0;
+    if (w.enter) return;
+    uint32_t pm = w.pm;
+    int32_t cur = w.cur;
+    if (pm == 0) {
+        int lv = w.depth;
+        while (pm == 0 && lv > 0) {
+            --lv;
+            pm = lv < 8 ? (uint32_t)(w.stk >> (8 * lv)) & 0xFFu : w.stk8;
+        }
+        if (pm == 0) return;
+        if (anc) {
+            cur = anc[lv * AS];
+        } else {
+            for (int l = w.depth; l > lv; --l) cur = sc.pid_up[cur];
+        }
+        const double2* nb = reinterpret_cast<const double2*>(sc.node_box + 6 * (size_t)cur);
+        pf.b0 = nb[0];
+        pf.b1 = nb[1];
+        pf.b2 = nb[2];
+        pf.lv = lv;
+        pf.kind = 2;
+    } else {
+        pf.kind = 1;
+    }
+    pf.cur = cur;
+    pf.pm = pm;
+    pf.ks = *reinterpret_cast<const int4*>(sc.node_slot + 8 * (size_t)cur + ((w.order >> (4 * __builtin_ctz(pm))) & 0xF));
+}
 template <int AS = 256>  // `anc`'s stride (the block's threads)
 RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w,
-                           LdsAncI32* anc = nullptr) {
+                           LdsAncI32* anc = nullptr, const SlotPF* pf = nullptr) {
     RT_DBG_TSTART(t_pop);
     uint32_t exist = 0;  // a node to enter: its existence mask (the root at a walk's start, or a descent)
     if (w.enter) {
         w.enter = 0;
         exist = (uint32_t)m.root_exist;
     } else {
-    if (w.pm == 0) {  // `cur` exhausted: resume at the nearest ancestor with children left
+    if (pf && pf->kind == 2) {  // the pop, its box fetched ahead (slot_prefetch)
+        w.cur = pf->cur;
+        w.depth = pf->lv;
+        w.pm = pf->pm;
+        w.path &= (1u << (3 * pf->lv)) - 1u;
+        w.mn[0] = pf->b0.x; w.mn[1] = pf->b0.y; w.mn[2] = pf->b1.x;
+        w.mx[0] = pf->b1.y; w.mx[1] = pf->b2.x; w.mx[2] = pf->b2.y;
+    } else if (w.pm == 0) {  // `cur` exhausted: resume at the nearest ancestor with children left
         int lv = w.depth;
         uint32_t pm = 0;
         while (pm == 0 && lv > 0) {
@@ -844,7 +920,7 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
         const int q = __builtin_ctz(w.pm);
         w.pm &= w.pm - 1u;
         oi = (w.order >> (4 * q)) & 0xF;
-        const int4 ks = kid_slot(sc, w.cur, oi);
+        const int4 ks = (pf && pf->kind != 0 && tries == 0) ? pf->ks : kid_slot(sc, w.cur, oi);
         if (!RT_SLOT_CULL || kid_tight_hit(m, ks, ray, inv)) {
             c = ks.x;
             break;
@@ -984,10 +1060,63 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         // next triangles are tested. Leaves are still tested in visiting order and the first leaf with
         // a hit ends the walk (a leaf the node walk found beyond it is dropped): the same result, in
         // fewer steps, with both parts of a step busy in most lanes.
+#if RT_WALK_HOIST == 2
+        // Triangle tests first, with the next node operation's loads issued before them: the open leaf's
+        // triangles and the pick's slot (and a pop's box) are fetched together at the step's start
+        // (slot_prefetch), so a step waits for one memory latency instead of two in a row. The node walk
+        // still runs one leaf ahead of the tests; a leaf it opens into a free cursor is tested from the
+        // next step. The same leaves in the same order: the same result.
+        {
+            const bool open = w.lpos < w.lend;
+            DevTri tr[kTrisPerStep];
+            if (open) {
+#pragma unroll
+                for (int j = 0; j < kTrisPerStep; ++j) tr[j] = sc.ltris[min(w.lpos + j, w.lend - 1)];
+            }
+            SlotPF pf;
+            pf.kind = 0;
+            if (!w.ndone) slot_prefetch<AS>(sc, w, anc, pf);
+            RT_DBG_TSTART(t_lt);
+            if (open) {
+                const int st = leaf_tris_loaded(sc, ray, w, tr, t, prim);
+                if (st == WALK_HIT) {
+                    RT_DBG_TEND(12, t_lt);
+                    return WALK_HIT;
+                }
+                if (st < 0 && w.nlf < w.nle) {  // leaf done without a hit: the buffered one is next
+                    w.lpos = w.nlf;
+                    w.lend = w.nle;
+                    w.best = -1;
+                    w.nle = w.nlf;
+                }
+            }
+            RT_DBG_TEND(12, t_lt);
+            if (!w.ndone && w.nlf >= w.nle && walk_node_slots<AS>(sc, m, ray, inv, w, anc, &pf) == WALK_MISS) w.ndone = 1;
+            return w.ndone && w.lpos >= w.lend && w.nlf >= w.nle ? WALK_MISS : WALK_RUN;
+        }
+#endif
+#if RT_WALK_HOIST == 1
+        // The open leaf's triangles are loaded BEFORE the node operation: while a leaf is open the node
+        // walk only fills the one-leaf buffer (nlf / nle), so the cursor stays as loaded and the slot load
+        // of the pick and the triangle loads are in flight together (one memory latency per step instead
+        // of two in a row). A leaf the node walk opens into a free cursor is tested from the next step:
+        // the same leaves in the same order, the same result.
+        const bool open = w.lpos < w.lend;
+        DevTri tr[kTrisPerStep];
+        if (open) {
+#pragma unroll
+            for (int j = 0; j < kTrisPerStep; ++j) tr[j] = sc.ltris[min(w.lpos + j, w.lend - 1)];
+        }
+#endif
         if (!w.ndone && w.nlf >= w.nle && walk_node_slots<AS>(sc, m, ray, inv, w, anc) == WALK_MISS) w.ndone = 1;
         RT_DBG_TSTART(t_lt);
+#if RT_WALK_HOIST == 1
+        if (open) {
+            const int st = leaf_tris_loaded(sc, ray, w, tr, t, prim);
+#else
         if (w.lpos < w.lend) {
             const int st = leaf_tris(sc, ray, w, t, prim);
+#endif
             if (st == WALK_HIT) {
                 RT_DBG_TEND(12, t_lt);
                 return WALK_HIT;
