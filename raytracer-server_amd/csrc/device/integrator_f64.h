@@ -165,7 +165,7 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
                          const Sink& sink = Sink()) {
     if (hr.obj < 0) return false;  // no hit: R = 0 (scene.rs:157, :175, :233)
     RT_DBG_REGION(6);
-    const DevObject& obj = sc.objects[hr.obj];
+    const DevObject& obj = object_at<C>(sc, hr.obj);
     V3 x, nrm;
     RT_DBG_TSTART(t_sf);
     surface<C>(sc, ps.ray, hr, &x, &nrm);
@@ -229,7 +229,7 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
         // (mirror vertices have no NEE)
         V3 lef = (RT_OPT_LEF && (!C::phong || obj.brdf == BRDF_DIFFUSE))
                      ? ld3(obj.lef)
-                     : mult(ld3(sc.objects[sc.light].emitted), brdf_eval<C>(obj, nrm, o, i));
+                     : mult(ld3(object_at<C>(sc, sc.light).emitted), brdf_eval<C>(obj, nrm, o, i));
         if (!is_zero(lef)) {  // a zero Le*f makes the term exactly 0: skip the shadow ray
             RT_DBG_REGION(9);
             double vis;

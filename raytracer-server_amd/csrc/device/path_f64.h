@@ -563,8 +563,9 @@ __shared__ unsigned long long s_dbg_time[8 * 16];
 #define RT_WALK_TIGHT 1  // A/B: 0 = visit every child whose octant box the ray hits (the reference's walk)
 #endif
 #ifndef RT_WALK_HOIST
-#define RT_WALK_HOIST 0  // A/B: the slot walk loads the open leaf's triangles before its node operation (1),
-                         // or tests them first with the node operation's loads fetched ahead (2)
+#define RT_WALK_HOIST 1  // the slot walk loads the open leaf's triangles before its node operation (1: unicorn
+                         // +2.4%, no spill at 254 VGPRs with the kernarg views), tests them first with the node
+                         // operation's loads fetched ahead (2: +2.1%), or after it (0) (profiles/r04_ab.log)
 #endif
 struct OctWalk {
     double mn[3], mx[3];  // box of `cur`
@@ -1246,13 +1247,37 @@ struct Cfg {
     static constexpr bool compact = (F & 8) != 0;  // scene fits the compact tables (DevScene)
     static constexpr bool bvh = (F & 16) != 0;     // RT_FLAG_MESH_NEAREST: nearest-triangle meshes via the BVH
     static constexpr bool nospec = (F & 32) != 0;  // no specular (mirror) object: the mirror paths compile out
+    static constexpr bool ldsobj = (F & 64) != 0;  // the kernel holds the object table in LDS (rt_lds_objects)
 };
+constexpr int kCfgLdsObj = 64;
+
+// The object table of compact scenes in LDS (16 x 208 B): a megakernel instantiated with Cfg bit 64
+// copies DevScene::objects here at its start (lds_objects_fill), so the shading's per-lane object reads
+// (hit object, light) are ds_reads instead of global loads. Only the kernels that reference it get it
+// allocated.
+__shared__ DevObject rt_lds_objects[kMaxCompactObjects];
+template <class C>
+RT_DEV const DevObject& object_at(const DevScene& sc, int i) {
+    if constexpr (C::ldsobj) return rt_lds_objects[i];
+    else return sc.objects[i];
+}
+RT_DEV void lds_objects_fill(const DevScene& sc) {
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(sc.objects);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(rt_lds_objects);
+    const int nw = sc.n_objects * (int)(sizeof(DevObject) / 8);
+    for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
 
 // Per-call view of the compact tables (scene_layout.h: CompactTab). The empty asm makes the pointer
 // opaque, so the scalar loads through it are issued inside each trace call instead of being
 // hoisted to the kernel entry, where the tables would hold ~100 SGPRs across the path loop.
 RT_DEV CTab* tables(const DevScene& sc) {
     uint64_t p = (uint64_t)(uintptr_t)sc.ctab;
+    // (uniform: readfirstlane keeps the asm's SGPR operand legal where the compiler holds it in a VGPR)
+    // (the builtin returns int: through uint32_t, or the low word's sign would fill the high word)
+    p = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)p) |
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32)) << 32);
     asm volatile("" : "+s"(p));
     return (CTab*)p;
 }
@@ -1346,12 +1371,12 @@ RT_DEV HitRec trace_closest(const DevScene& sc, const Ray& ray) {
             double t;
             int prim = -1;
             const double tmax = h.obj >= 0 ? h.t : INFINITY;
-            if (object_t<C>(sc, sc.objects[idx], ray, inv, &t, &prim, tmax)) consider(h, t, idx, prim);
+            if (object_t<C>(sc, object_at<C>(sc, idx), ray, inv, &t, &prim, tmax)) consider(h, t, idx, prim);
         }
         return h;
     }
     for (int i = 0; i < sc.n_objects; ++i) {
-        const DevObject& o = sc.objects[i];
+        const DevObject& o = object_at<C>(sc, i);
         double t;
         int prim = -1;
         if (object_t<C>(sc, o, ray, inv, &t, &prim)) {
@@ -1364,7 +1389,7 @@ RT_DEV HitRec trace_closest(const DevScene& sc, const Ray& ray) {
 // Hit position and facing normal, computed exactly as the intersect routines build their Hit.
 template <class C>
 RT_DEV void surface(const DevScene& sc, const Ray& ray, const HitRec& h, V3* pos, V3* n) {
-    const DevObject& o = sc.objects[h.obj];
+    const DevObject& o = object_at<C>(sc, h.obj);
     if (o.geom == GEOM_SPHERE) {
         V3 p = eval(ray, h.t);
         V3 nn = norm(p - ld3(o.pos));
@@ -1433,7 +1458,7 @@ RT_DEV bool visible_ray(const DevScene& sc, V3 y, const Ray& r, double dist) {
         for (int i = 0; i < T->n_gen; ++i) {
             double t;
             int prim;
-            if (object_t<C>(sc, sc.objects[T->gen_idx[i]], r, inv, &t, &prim, dist) && !(t + ERR_MARGIN >= dist))
+            if (object_t<C>(sc, object_at<C>(sc, T->gen_idx[i]), r, inv, &t, &prim, dist) && !(t + ERR_MARGIN >= dist))
                 return false;
         }
         return true;
@@ -1441,7 +1466,7 @@ RT_DEV bool visible_ray(const DevScene& sc, V3 y, const Ray& r, double dist) {
     const RayInv inv = make_inv(r.d);
     for (int pass = 0; pass < (C::mesh ? 2 : 1); ++pass) {
         for (int i = 0; i < sc.n_objects; ++i) {
-            const DevObject& o = sc.objects[i];
+            const DevObject& o = object_at<C>(sc, i);
             if ((o.geom == GEOM_MESH) != (pass == 1)) continue;
             double t;
             int prim;
@@ -1475,7 +1500,7 @@ RT_DEV HitRec trace_analytic(const DevScene& sc, const Ray& ray, const RayInv& i
     }
     for (int i = 0; i < T->n_gen; ++i) {
         const int idx = T->gen_idx[i];
-        const DevObject& o = sc.objects[idx];
+        const DevObject& o = object_at<C>(sc, idx);
         double t;
         if (analytic_t(o, ray, inv, &t)) consider(h, t, idx, -1);
     }
@@ -1487,7 +1512,7 @@ RT_DEV void trace_meshes(const DevScene& sc, const Ray& ray, const RayInv& inv, 
     CTab* T = tables(sc);
     for (int i = 0; i < T->n_gen; ++i) {
         const int idx = T->gen_idx[i];
-        const DevObject& o = sc.objects[idx];
+        const DevObject& o = object_at<C>(sc, idx);
         if (o.geom != GEOM_MESH) continue;
         double t;
         int prim = -1;
@@ -1530,7 +1555,7 @@ RT_DEV uint32_t mesh_near_mask(const DevScene& sc, const Ray& ray, const RayInv&
     CTab* T = tables(sc);
     uint32_t mask = 0;
     for (int i = 0; i < T->n_gen; ++i) {
-        const DevObject& o = sc.objects[T->gen_idx[i]];
+        const DevObject& o = object_at<C>(sc, T->gen_idx[i]);
         if (o.geom == GEOM_MESH && sc.meshes[o.mesh].n_nodes > 0) {
             const DevMesh& m = sc.meshes[o.mesh];
 #if RT_NEAR32
@@ -1568,7 +1593,7 @@ RT_DEV bool visible_analytic(const DevScene& sc, V3 y, const Ray& r, const RayIn
     }
     if (occluded) return false;
     for (int i = 0; i < T->n_gen; ++i) {
-        const DevObject& o = sc.objects[T->gen_idx[i]];
+        const DevObject& o = object_at<C>(sc, T->gen_idx[i]);
         double t;
         if (analytic_t(o, r, inv, &t) && !(t + ERR_MARGIN >= dist)) return false;
     }
@@ -1579,7 +1604,7 @@ RT_DEV bool mesh_occludes(const DevScene& sc, const Ray& r, const RayInv& inv, d
     CTab* T = tables(sc);
     const double ERR_MARGIN = 0.001;
     for (int i = 0; i < T->n_gen; ++i) {
-        const DevObject& o = sc.objects[T->gen_idx[i]];
+        const DevObject& o = object_at<C>(sc, T->gen_idx[i]);
         if (o.geom != GEOM_MESH) continue;
         double t;
         int prim;
@@ -1659,7 +1684,7 @@ RT_DEV void brdf_sample(const DevObject& o, V3 n, V3 out, Rng& rng, V3* in, doub
 // ---------------------------------------------------------------- light (geometry.rs:573-595)
 template <class C>
 RT_DEV void light_sample(const DevScene& sc, Rng& rng, V3* y, V3* ny, double* pdf) {
-    const DevObject& L = sc.objects[sc.light];
+    const DevObject& L = object_at<C>(sc, sc.light);
     if (!C::mesh || L.geom == GEOM_SPHERE) {
         double xi1 = rng.uniform(), xi2 = rng.uniform();
         double z = 2. * xi1 - 1.;

@@ -26,6 +26,31 @@ __device__ __forceinline__ long wave_ticket(uint32_t* counter, bool want) {
     return want ? (long)base + __popcll(below) : -1;
 }
 
+// The megakernels' own (DevScene, RenderArgs) arguments, read in place in the kernel-argument segment
+// through an opaque constant-space pointer: every use is a scalar load (a K$ hit) issued where the
+// value is needed. Held as values, their ~100 SGPRs live across the whole path loop and the register
+// allocator spills them to VGPR lanes (v_writelane at entry, v_readlane at each use: VALU issue slots
+// and SGPR hazard nops in a VALU-bound loop; 54 SGPR + 4 VGPR spills in k_megakernel_f64<8,4>). The
+// megakernels take DevScene and RenderArgs as their first two arguments: by the AMDGPU kernarg layout
+// at offset 0 and at sizeof(DevScene) rounded up to RenderArgs' alignment (248: the code objects'
+// .args metadata). RT_KARG_VIEW=0 builds keep the by-value arguments (A/B).
+#ifndef RT_KARG_VIEW
+#define RT_KARG_VIEW 1
+#endif
+typedef const __attribute__((address_space(4))) char KargByte;
+constexpr size_t kKargArgsOffset = (sizeof(DevScene) + alignof(RenderArgs) - 1) / alignof(RenderArgs) * alignof(RenderArgs);
+static_assert(kKargArgsOffset == 248, "DevScene / RenderArgs kernarg layout changed: check the .args metadata");
+__device__ __forceinline__ KargByte* karg_base() {
+    KargByte* p = (KargByte*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));  // opaque: no value is hoisted to the kernel entry and held in SGPRs
+    return p;
+}
+__device__ __forceinline__ const DevScene& karg_scene() {
+    return *(const DevScene*)(const __attribute__((address_space(4))) DevScene*)karg_base();
+}
+__device__ __forceinline__ const RenderArgs& karg_render_args() {
+    return *(const RenderArgs*)(const __attribute__((address_space(4))) RenderArgs*)(karg_base() + kKargArgsOffset);
+}
 // Adds the wave's vertex counts to *counter and zeroes them. All 64 lanes must call it together.
 __device__ __forceinline__ void flush_count(unsigned long long* counter, uint32_t& n) {
     if (!counter) return;

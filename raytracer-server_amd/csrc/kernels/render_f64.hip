@@ -37,23 +37,19 @@ typedef __attribute__((address_space(3))) uint64_t LdsU64;
 #endif
 
 template <int F, int W>
-__global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
+__global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, RenderArgs a_g, double* __restrict__ sub_buf,
                                                           uint32_t* next_sub, long nsub, int refill) {
-    using C = Cfg<F>;
     // Compact scenes (<= kMaxCompactObjects objects): the object table is copied into LDS, so the
     // shading's per-lane object reads (hit object, light) are ds_reads instead of global loads.
-    DevScene sc = sc_g;
-#if RT_OPT_LDSOBJ
-    __shared__ DevObject s_objs[C::compact ? kMaxCompactObjects : 1];
-    if constexpr (C::compact) {
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(sc_g.objects);
-        uint64_t* dst = reinterpret_cast<uint64_t*>(s_objs);
-        const int nw = sc_g.n_objects * (int)(sizeof(DevObject) / 8);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-        __syncthreads();
-        sc.objects = s_objs;
-    }
+    using C = Cfg<F | ((RT_OPT_LDSOBJ && (F & 8)) ? kCfgLdsObj : 0)>;
+#if RT_KARG_VIEW
+    const DevScene& sc = karg_scene();  // the arguments read in place (megakernel_common.h)
+    const RenderArgs& a = karg_render_args();
+#else
+    const DevScene& sc = sc_g;
+    const RenderArgs& a = a_g;
 #endif
+    if constexpr (C::ldsobj) lds_objects_fill(sc);
     // Rarely touched per-lane state lives in LDS (one column per thread; VGPRs are the limit at 4
     // waves/SIMD): the subpixel accumulator (once per sample) and the camera-sample buffer — a ring
     // of kCamDepth next samples (camera ray + RNG state) per lane, computed ahead in passes the whole

@@ -290,19 +290,18 @@ RT_DEV void process_queries(const DevScene& sc, const int32_t* cnt_c, const int3
 }  // namespace
 
 template <int F, int W>
-__global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
+__global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, RenderArgs a_g, double* __restrict__ sub_buf,
                                                                 uint32_t* next_sub, long nsub) {
-    using C = Cfg<F>;
+    using C = Cfg<F | kCfgLdsObj>;  // the object table in LDS (path_f64.h rt_lds_objects)
     static_assert(C::mesh && C::compact && !C::bvh, "flat-mesh kernel: compact scenes, octree meshes");
-    DevScene sc = sc_g;
-    __shared__ DevObject s_objs[kMaxCompactObjects];
-    {
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(sc_g.objects);
-        uint64_t* dst = reinterpret_cast<uint64_t*>(s_objs);
-        const int nw = sc_g.n_objects * (int)(sizeof(DevObject) / 8);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-        sc.objects = s_objs;
-    }
+#if RT_KARG_VIEW
+    const DevScene& sc = karg_scene();  // the arguments read in place (megakernel_common.h)
+    const RenderArgs& a = karg_render_args();
+#else
+    const DevScene& sc = sc_g;
+    const RenderArgs& a = a_g;
+#endif
+    lds_objects_fill(sc);
     // per lane (one column per thread): subpixel accumulator; the closest-hit query ray (o, d), the
     // shadow query ray (o, d, |y - x|); results per (mesh, lane); queues per (kind, parity, mesh):
     // the closest queries of iteration i and the shadow queries of i - 1 are in flight together
@@ -405,7 +404,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
             CTab* T = tables(sc);
             for (int g = 0; g < T->n_gen; ++g) {  // Scene::trace_ray's loop over the meshes (ties: lower index)
                 const int idx = T->gen_idx[g];
-                const DevObject& o = sc.objects[idx];
+                const DevObject& o = object_at<C>(sc, idx);
                 if (o.geom == GEOM_MESH && ((qmask >> o.mesh) & 1u)) {
                     const int p = s_rp[o.mesh * kBlk + tid];
                     if (p >= 0) consider(h, s_rt[o.mesh * kBlk + tid], idx, p);
@@ -510,19 +509,18 @@ constexpr int kFpRing = 512;  // per mesh: at most 256 closest-hit + 256 shadow 
 #endif
 
 template <int F, int W>
-__global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
+__global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g, RenderArgs a_g, double* __restrict__ sub_buf,
                                                                  uint32_t* next_sub, long nsub, int pool_min, int refill) {
-    using C = Cfg<F>;
+    using C = Cfg<F | kCfgLdsObj>;  // the object table in LDS (path_f64.h rt_lds_objects)
     static_assert(C::mesh && C::compact && !C::bvh, "flat-mesh kernel: compact scenes, octree meshes");
-    DevScene sc = sc_g;
-    __shared__ DevObject s_objs[kMaxCompactObjects];
-    {
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(sc_g.objects);
-        uint64_t* dst = reinterpret_cast<uint64_t*>(s_objs);
-        const int nw = sc_g.n_objects * (int)(sizeof(DevObject) / 8);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-        sc.objects = s_objs;
-    }
+#if RT_KARG_VIEW
+    const DevScene& sc = karg_scene();  // the arguments read in place (megakernel_common.h)
+    const RenderArgs& a = karg_render_args();
+#else
+    const DevScene& sc = sc_g;
+    const RenderArgs& a = a_g;
+#endif
+    lds_objects_fill(sc);
     // per lane (one column per thread): subpixel accumulator; the closest-hit query ray (o, d), the
     // shadow query ray (o, d, |y - x|); results per (mesh, lane); queries outstanding per lane
     // The closest-hit and the shadow query of a lane are issued in the same iteration from the same
@@ -645,7 +643,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                 CTab* T = tables(sc);
                 for (int g = 0; g < T->n_gen; ++g) {  // Scene::trace_ray's loop over the meshes (ties: lower index)
                     const int idx = T->gen_idx[g];
-                    const DevObject& o = sc.objects[idx];
+                    const DevObject& o = object_at<C>(sc, idx);
                     if (o.geom == GEOM_MESH && ((qmask >> o.mesh) & 1u)) {
                         const int p = s_rp[o.mesh * kBlk + tid];
                         if (p != 0xFF) consider(h, s_rt[o.mesh * kBlk + tid], idx, sc.meshes[o.mesh].tri_base + p);

@@ -28,7 +28,7 @@ template <class C, bool S>
 RT_DEV bool next_mesh_walk(const DevScene& sc, const Ray& r, const RayInv& inv, double tmax, int& g, int& mi,
                            OctWalk& w) {
     for (++g; g < tables(sc)->n_gen; ++g) {
-        const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
+        const DevObject& o = object_at<C>(sc, tables(sc)->gen_idx[g]);
         if (o.geom == GEOM_MESH && walk_begin<S>(sc, sc.meshes[o.mesh], r, inv, tmax, w)) {
             mi = o.mesh;
             return true;
@@ -42,7 +42,7 @@ template <class C, bool S>
 RT_DEV bool next_mesh_walk_near(const DevScene& sc, const Ray& r, const RayInv& inv, double tmax, int& g, int& mi,
                                 OctWalk& w, uint32_t near) {
     for (++g; g < tables(sc)->n_gen; ++g) {
-        const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
+        const DevObject& o = object_at<C>(sc, tables(sc)->gen_idx[g]);
         if (o.geom == GEOM_MESH && ((near >> o.mesh) & 1u) && walk_begin<S>(sc, sc.meshes[o.mesh], r, inv, tmax, w, false)) {
             mi = o.mesh;
             return true;
@@ -161,7 +161,7 @@ template <class C>
 RT_DEV bool next_mesh_walk_bvh(const DevScene& sc, const Ray& r, const RayInv& inv, double tmax, int& g, int& mi,
                                BvhWalk& w) {
     for (++g; g < tables(sc)->n_gen; ++g) {
-        const DevObject& o = sc.objects[tables(sc)->gen_idx[g]];
+        const DevObject& o = object_at<C>(sc, tables(sc)->gen_idx[g]);
         if (o.geom != GEOM_MESH) continue;
         const DevMesh& m = sc.meshes[o.mesh];
         if (m.bvh_n > 0 && near_box(m.cull_box, r, inv, m.cull_pad, tmax)) {
@@ -454,25 +454,21 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
 }
 
 template <int F, int W, int P, bool S, int B = P ? kPoolThreads : 256>
-__global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, RenderArgs a, double* __restrict__ sub_buf,
+__global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, RenderArgs a_g, double* __restrict__ sub_buf,
                                                                uint32_t* next_sub, long nsub, int ksteps, int wmin,
                                                                int refill, int pool_min, int pool_vmin) {
-    using C = Cfg<F>;
+    using C = Cfg<F | (RT_OPT_LDSOBJ ? kCfgLdsObj : 0)>;
     static_assert(C::mesh && C::compact, "mesh megakernel needs the compact tables");
     static_assert(B % 64 == 0 && B <= 512, "whole waves, at most 8 (path_f64.h: the diagnostic builds' per-wave LDS)");
-    // object table in LDS, as in k_megakernel_f64 (2 blocks per CU: 2 x 78 KB of LDS)
-    DevScene sc = sc_g;
-#if RT_OPT_LDSOBJ
-    __shared__ DevObject s_objs[kMaxCompactObjects];
-    {
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(sc_g.objects);
-        uint64_t* dst = reinterpret_cast<uint64_t*>(s_objs);
-        const int nw = sc_g.n_objects * (int)(sizeof(DevObject) / 8);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-        __syncthreads();
-        sc.objects = s_objs;
-    }
+    // object table in LDS, as in k_megakernel_f64; the arguments read in place (megakernel_common.h)
+#if RT_KARG_VIEW
+    const DevScene& sc = karg_scene();
+    const RenderArgs& a = karg_render_args();
+#else
+    const DevScene& sc = sc_g;
+    const RenderArgs& a = a_g;
 #endif
+    if constexpr (C::ldsobj) lds_objects_fill(sc);
     __shared__ double s_park_d[(P ? kPark2D : kParkD) * B];
     // pool: + the slot walk's ancestor ids (walk_node_slots)
     __shared__ int32_t s_park_i[(P ? kPark2I + (S ? kSlotAncLevels : 0) : kParkI) * B];
