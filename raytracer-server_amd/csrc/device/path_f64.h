@@ -292,9 +292,26 @@ RT_DEV bool plane_t(const DevObject& o, const Ray& ray, const RayInv& inv, doubl
 }
 // Triangle::intersect (geometry.rs:637-670) on the precomputed (a, ab, ac, n); TR = DevTri in any
 // address space (flat_query reads its triangles through a constant-address-space pointer: s_load).
+// The triangle's unit normal: stored (DevTri), or recomputed for a 72-B leaf copy with the host's own
+// operations (rt_api.cpp: Triangle::normal = (c - a).cross(b - a).norm()), so the same bits.
+template <class TR>
+RT_DEV V3 tri_normal(const TR& tr) {
+    if constexpr (sizeof(TR) == sizeof(DevTri)) {
+        return ld3(tr.n);
+    } else {
+        const V3 ab = ld3(tr.ab), ac = ld3(tr.ac);
+        const V3 cr = v3(ac.y * ab.z - ac.z * ab.y, ac.z * ab.x - ac.x * ab.z, ac.x * ab.y - ac.y * ab.x);
+        const double mg = sqrt_rn(cr.x * cr.x + cr.y * cr.y + cr.z * cr.z);
+        if (wave_all(rcp_safe(mg))) {
+            const double y = rcp_rn(mg);
+            return v3(qdiv(cr.x, mg, y), qdiv(cr.y, mg, y), qdiv(cr.z, mg, y));
+        }
+        return v3(cr.x / mg, cr.y / mg, cr.z / mg);
+    }
+}
 template <class TR>
 RT_DEV bool tri_t(const TR& tr, const Ray& ray, double* tout) {
-    V3 n = ld3(tr.n);
+    V3 n = tri_normal(tr);
     if (fabs(dot(n, ray.d)) < 0.0001) return false;
     V3 ab = ld3(tr.ab), ac = ld3(tr.ac);
     V3 b = ray.o - ld3(tr.a);
@@ -701,7 +718,7 @@ RT_DEV int leaf_tris(const DevScene& sc, const Ray& ray, OctWalk& w, double* t, 
     // tests |n . d| and only then its other 72 B, and the next triangle only after that, i.e. four
     // dependent trips to L2 / the Infinity Cache per step. Entries past the leaf's end are clamped
     // to its last one (loaded, never tested).
-    DevTri tr[kTrisPerStep];
+    LeafTri tr[kTrisPerStep];
 #pragma unroll
     for (int j = 0; j < kTrisPerStep; ++j) {
         const int e = max(0, min(w.lpos + j, w.lend - 1));
@@ -723,7 +740,7 @@ RT_DEV int leaf_tris(const DevScene& sc, const Ray& ray, OctWalk& w, double* t, 
 #if RT_LTRI_INDEX
             const DevTri& trj = sc.tris[sc.ltri_id[w.lpos]];  // leaf list = triangle indices (3.6 MB table)
 #else
-            const DevTri& trj = sc.ltris[w.lpos];  // leaf list = triangle copies (18 MB for the unicorn)
+            const LeafTri& trj = sc.ltris[w.lpos];  // leaf list = triangle copies (18 MB for the unicorn)
 #endif
             if (tri_t(trj, ray, &tt) && (w.best < 0 || tt < w.bt)) {
 #endif
@@ -742,7 +759,7 @@ RT_DEV int leaf_tris(const DevScene& sc, const Ray& ray, OctWalk& w, double* t, 
     return -1;
 }
 // The tests of leaf_tris on triangles already loaded (the slot walk's hoisted loads, walk_step<true>).
-RT_DEV int leaf_tris_loaded(const DevScene& sc, const Ray& ray, OctWalk& w, const DevTri* tr, double* t, int* prim) {
+RT_DEV int leaf_tris_loaded(const DevScene& sc, const Ray& ray, OctWalk& w, const LeafTri* tr, double* t, int* prim) {
 #pragma unroll
     for (int j = 0; j < kTrisPerStep; ++j) {
         if (w.lpos < w.lend) {
@@ -806,6 +823,9 @@ constexpr int kSlotAncLevels = 9;
 #endif
 #ifndef RT_SLOT_CULL
 #define RT_SLOT_CULL 1  // A/B: 0 = the slot walk without the subtree-bounds test
+#endif
+#ifndef RT_SLOT_PAIR
+#define RT_SLOT_PAIR 1  // a pick loads the slots of the next two candidates together (1: unicorn +0.7%, r04j) or one by one (0)
 #endif  // the deepest parents sit at depth 8 (MAX_DEPTH 10, root depth 1)
 // What the next node operation will load, fetched ahead (RT_WALK_HOIST=2: at the start of the step,
 // before its triangle tests): kind 1 = a pick at `cur` (its first candidate's slot), kind 2 = a pop to
@@ -917,6 +937,36 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
     // picks per step (a culled pick is as if the reference found nothing below that child)
     int32_t c = kKidEmpty;
     uint32_t oi = 0;
+#if RT_SLOT_PAIR
+    if (!pf) {
+        // both candidates' slots loaded at once (one row of node_slot: the same 128-byte line), so a
+        // culled first pick does not wait a second memory latency for the second
+        const uint32_t pm1 = w.pm & (w.pm - 1u);
+        const uint32_t oi1 = (w.order >> (4 * __builtin_ctz(w.pm))) & 0xF;
+        const uint32_t oi2 = pm1 ? (w.order >> (4 * __builtin_ctz(pm1))) & 0xF : oi1;
+        const int4 ks1 = kid_slot(sc, w.cur, oi1);
+        const int4 ks2 = kid_slot(sc, w.cur, oi2);
+        w.pm = pm1;
+        oi = oi1;
+        if (!RT_SLOT_CULL || kid_tight_hit(m, ks1, ray, inv)) {
+            c = ks1.x;
+        } else {
+            RT_DBG(6);
+            if (w.pm == 0) {  // nothing picked in this step
+                RT_DBG_TEND(14, t_pick);
+                return WALK_RUN;
+            }
+            w.pm &= w.pm - 1u;
+            oi = oi2;
+            if (!kid_tight_hit(m, ks2, ray, inv)) {
+                RT_DBG(6);
+                RT_DBG_TEND(14, t_pick);
+                return WALK_RUN;
+            }
+            c = ks2.x;
+        }
+    } else
+#endif
     for (int tries = 0; tries < 2; ++tries) {
         const int q = __builtin_ctz(w.pm);
         w.pm &= w.pm - 1u;
@@ -1069,7 +1119,7 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         // next step. The same leaves in the same order: the same result.
         {
             const bool open = w.lpos < w.lend;
-            DevTri tr[kTrisPerStep];
+            LeafTri tr[kTrisPerStep];
             if (open) {
 #pragma unroll
                 for (int j = 0; j < kTrisPerStep; ++j) tr[j] = sc.ltris[min(w.lpos + j, w.lend - 1)];
@@ -1103,7 +1153,7 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         // of two in a row). A leaf the node walk opens into a free cursor is tested from the next step:
         // the same leaves in the same order, the same result.
         const bool open = w.lpos < w.lend;
-        DevTri tr[kTrisPerStep];
+        LeafTri tr[kTrisPerStep];
         if (open) {
 #pragma unroll
             for (int j = 0; j < kTrisPerStep; ++j) tr[j] = sc.ltris[min(w.lpos + j, w.lend - 1)];

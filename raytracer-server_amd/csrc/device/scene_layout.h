@@ -122,6 +122,19 @@ RT_LAYOUT_FN uint32_t slot_exist(int32_t e) { return (uint32_t)e >> 23; }
 struct DevTri {
     double a[3], ab[3], ac[3], n[3];
 };
+// The octree leaves' triangle copies (DevScene::ltris): DevTri, or in RT_LTRI72 builds 72 B without the
+// normal, which the walk's test recomputes with the host's operations (tri_normal, path_f64.h).
+#ifndef RT_LTRI72
+#define RT_LTRI72 0
+#endif
+struct DevTri72 {
+    double a[3], ab[3], ac[3];
+};
+#if RT_LTRI72
+typedef DevTri72 LeafTri;
+#else
+typedef DevTri LeafTri;
+#endif
 
 // Compact per-type object tables, passed in the kernel arguments so the trace loops are unrolled
 // and their operands live in scalar registers (no per-object loads or type branches). Objects keep
@@ -183,7 +196,7 @@ struct DevScene {
     const int32_t* node_kids;   // [node][8], see kid_leaf (leaf triangle ranges inline)
     const int2* node_up;        // [node] {parent, slot}
     const int2* leaf_span;      // [leaf] {first ltri, count}
-    const DevTri* ltris;        // RT_LTRI_INDEX=0 builds only: leaf triangle lists as copies, in leaf order
+    const LeafTri* ltris;       // RT_LTRI_INDEX=0 builds only: leaf triangle lists as copies, in leaf order
                                 // (the reference's leaves hold (index, Triangle) copies, geometry.rs:1131-1137)
     const int32_t* ltri_id;     // [ltri] leaf triangle lists as global triangle indices into `tris`, in leaf
                                 // order (the walk's triangles and the hit's `prim`)

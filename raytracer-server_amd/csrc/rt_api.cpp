@@ -49,7 +49,7 @@ struct Packed {
     std::vector<int32_t> kids;   // [node][8]
     std::vector<int2> up;        // [node]
     std::vector<int2> leaves;    // [leaf] {first ltri, count}
-    std::vector<rt::DevTri> ltris;
+    std::vector<rt::LeafTri> ltris;
     std::vector<int32_t> ltri_id;
     std::vector<rt::DevTri> tris;
     std::vector<double> cum_area;
@@ -333,7 +333,14 @@ int pack_scene(rt_scene* s) {
             for (int32_t r = 0; r < oc.leaf_cnt[i]; ++r) {
                 const int32_t t = oc.refs[oc.leaf_off[i] + r];
 #if !RT_LTRI_INDEX
-                p.ltris.push_back(p.tris[dm.tri_base + t]);
+                const rt::DevTri& lt = p.tris[dm.tri_base + t];
+#if RT_LTRI72
+                rt::LeafTri l72{};
+                for (int k = 0; k < 3; ++k) { l72.a[k] = lt.a[k]; l72.ab[k] = lt.ab[k]; l72.ac[k] = lt.ac[k]; }
+                p.ltris.push_back(l72);
+#else
+                p.ltris.push_back(lt);
+#endif
 #endif
                 p.ltri_id.push_back(dm.tri_base + t);
             }
@@ -711,7 +718,7 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.node_kids = (const int32_t*)(b + o_kids);
         ds.node_up = (const int2*)(b + o_up);
         ds.leaf_span = (const int2*)(b + o_leaf);
-        ds.ltris = (const rt::DevTri*)(b + o_ltri);
+        ds.ltris = (const rt::LeafTri*)(b + o_ltri);
         ds.ltri_id = (const int32_t*)(b + o_lid);
         ds.tris = (const rt::DevTri*)(b + o_tris);
         ds.tri_cum_area = (const double*)(b + o_cum);
