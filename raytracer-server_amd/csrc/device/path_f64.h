@@ -199,6 +199,9 @@ RT_DEV double div_y(double a, const Ray& r, const RayInv& v) { return qdiv(a, r.
 RT_DEV double div_z(double a, const Ray& r, const RayInv& v) { return qdiv(a, r.d.z, v.rz); }
 
 // ---------------------------------------------------------------- RNG v2
+#ifndef RT_RNG32
+#define RT_RNG32 0
+#endif
 // One xoroshiro128++ stream per camera sample, seeded by Philox4x32-10(key = seed,
 // counter = (pixel, sample, 0, subpixel)); consumed in the reference's draw order along the path.
 struct Rng {
@@ -224,6 +227,27 @@ struct Rng {
         if ((s0 | s1) == 0) s0 = 1;
     }
     static RT_DEV uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+#if RT_RNG32
+    // A/B (RNG v3 candidate): xoshiro128++ on the same 128 state bits (x0..x3 = the 32-bit halves of
+    // s0, s1), one 32-bit output per draw, uniform = k * 2^-32
+    static RT_DEV uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+    RT_DEV uint32_t next32() {
+        uint32_t x0 = (uint32_t)s0, x1 = (uint32_t)(s0 >> 32), x2 = (uint32_t)s1, x3 = (uint32_t)(s1 >> 32);
+        const uint32_t r = rotl32(x0 + x3, 7) + x0;
+        const uint32_t t = x1 << 9;
+        x2 ^= x0;
+        x3 ^= x1;
+        x1 ^= x2;
+        x0 ^= x3;
+        x2 ^= t;
+        x3 = rotl32(x3, 11);
+        s0 = (uint64_t)x0 | ((uint64_t)x1 << 32);
+        s1 = (uint64_t)x2 | ((uint64_t)x3 << 32);
+        return r;
+    }
+    RT_DEV double uniform() { return (double)next32() * 0x1p-32; }
+    RT_DEV bool below53(uint64_t thr) { return ((uint64_t)next32() << 21) < thr; }
+#endif
     RT_DEV uint64_t next() {  // xoroshiro128++
         uint64_t a = s0, b = s1;
         uint64_t r = rotl(a + b, 17) + a;
@@ -232,6 +256,7 @@ struct Rng {
         s1 = rotl(b, 28);
         return r;
     }
+#if !RT_RNG32
 #ifndef RT_OPT_UNIF
 #define RT_OPT_UNIF 0  // A/B: 1 = two 32-bit conversions and one FMA (same bits; measured 0.6% slower on
                        // cornell_box, profiles/r02_ab.log r02z), 0 = the u64 -> f64 conversion
@@ -249,6 +274,7 @@ struct Rng {
     // uniform() < p for p = thr * 2^-53 (thr an integer <= 2^53): the draw is v * 2^-53 exactly, so
     // the comparison is v < thr, with no conversion (Russian roulette, scene.rs:173/:231)
     RT_DEV bool below53(uint64_t thr) { return (next() >> 11) < thr; }
+#endif
 };
 // Russian-roulette thresholds as 53-bit integers: p = 1 (depth <= MAX_BOUNCES) and p = 0.9, whose
 // double is M * 2^-53 for an integer M (0.9 lies in [0.5, 1))
