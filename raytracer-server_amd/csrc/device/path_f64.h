@@ -785,7 +785,10 @@ RT_DEV int leaf_tris(const DevScene& sc, const Ray& ray, OctWalk& w, double* t, 
     return -1;
 }
 // The tests of leaf_tris on triangles already loaded (the slot walk's hoisted loads, walk_step<true>).
-RT_DEV int leaf_tris_loaded(const DevScene& sc, const Ray& ray, OctWalk& w, const LeafTri* tr, double* t, int* prim) {
+// tid (RT_LTRI_ID_HOIST): the triangles' global ids, loaded with them; w.best then holds the best
+// triangle's id itself, so a hit needs no dependent ltri_id load at the leaf's end.
+RT_DEV int leaf_tris_loaded(const DevScene& sc, const Ray& ray, OctWalk& w, const LeafTri* tr, double* t, int* prim,
+                            const int32_t* tid = nullptr) {
 #pragma unroll
     for (int j = 0; j < kTrisPerStep; ++j) {
         if (w.lpos < w.lend) {
@@ -793,7 +796,7 @@ RT_DEV int leaf_tris_loaded(const DevScene& sc, const Ray& ray, OctWalk& w, cons
             double tt;
             if (tri_t(tr[j], ray, &tt) && (w.best < 0 || tt < w.bt)) {
                 w.bt = tt;
-                w.best = w.lpos;
+                w.best = tid ? tid[j] : w.lpos;
             }
             ++w.lpos;
         }
@@ -801,7 +804,7 @@ RT_DEV int leaf_tris_loaded(const DevScene& sc, const Ray& ray, OctWalk& w, cons
     if (w.lpos < w.lend) return WALK_RUN;
     if (w.best >= 0) {
         *t = w.bt;
-        *prim = sc.ltri_id[w.best];
+        *prim = tid ? w.best : sc.ltri_id[w.best];
         return WALK_HIT;
     }
     return -1;
@@ -849,6 +852,9 @@ constexpr int kSlotAncLevels = 9;
 #endif
 #ifndef RT_SLOT_CULL
 #define RT_SLOT_CULL 1  // A/B: 0 = the slot walk without the subtree-bounds test
+#endif
+#ifndef RT_LTRI_ID_HOIST
+#define RT_LTRI_ID_HOIST 1  // the hoisted triangle loads also load the triangles' ids (leaf_tris_loaded: unicorn +1.5%, r04o), or not (0)
 #endif
 #ifndef RT_SLOT_PAIR
 #define RT_SLOT_PAIR 1  // a pick loads the slots of the next two candidates together (1: unicorn +0.7%, r04j) or one by one (0)
@@ -1127,7 +1133,9 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
 // Slots = the slot walk (walk_node_slots, RT_WALK_TIGHT) or the node_kids walk (walk_node); both give
 // the reference's result. (The wavefront's persistent walk kernels use the node_kids walk: the slot
 // walk inlined there trips an AMDGPU backend error, "illegal VGPR to SGPR copy", in ROCm 7.2.)
-template <bool Slots = (RT_WALK_TIGHT != 0), int AS = 256>
+// Hoist: RT_WALK_HOIST's modes (below); the Phong / mesh-light instances of the walk pool pass 0, where
+// the hoisted triangles' registers would spill.
+template <bool Slots = (RT_WALK_TIGHT != 0), int AS = 256, int Hoist = RT_WALK_HOIST>
 RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w, double* t,
                      int* prim, LdsAncI32* anc = nullptr) {
     RT_DBG(5);
@@ -1137,63 +1145,34 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         // next triangles are tested. Leaves are still tested in visiting order and the first leaf with
         // a hit ends the walk (a leaf the node walk found beyond it is dropped): the same result, in
         // fewer steps, with both parts of a step busy in most lanes.
-#if RT_WALK_HOIST == 2
-        // Triangle tests first, with the next node operation's loads issued before them: the open leaf's
-        // triangles and the pick's slot (and a pop's box) are fetched together at the step's start
-        // (slot_prefetch), so a step waits for one memory latency instead of two in a row. The node walk
-        // still runs one leaf ahead of the tests; a leaf it opens into a free cursor is tested from the
-        // next step. The same leaves in the same order: the same result.
-        {
-            const bool open = w.lpos < w.lend;
-            LeafTri tr[kTrisPerStep];
-            if (open) {
-#pragma unroll
-                for (int j = 0; j < kTrisPerStep; ++j) tr[j] = sc.ltris[min(w.lpos + j, w.lend - 1)];
-            }
-            SlotPF pf;
-            pf.kind = 0;
-            if (!w.ndone) slot_prefetch<AS>(sc, w, anc, pf);
-            RT_DBG_TSTART(t_lt);
-            if (open) {
-                const int st = leaf_tris_loaded(sc, ray, w, tr, t, prim);
-                if (st == WALK_HIT) {
-                    RT_DBG_TEND(12, t_lt);
-                    return WALK_HIT;
-                }
-                if (st < 0 && w.nlf < w.nle) {  // leaf done without a hit: the buffered one is next
-                    w.lpos = w.nlf;
-                    w.lend = w.nle;
-                    w.best = -1;
-                    w.nle = w.nlf;
-                }
-            }
-            RT_DBG_TEND(12, t_lt);
-            if (!w.ndone && w.nlf >= w.nle && walk_node_slots<AS>(sc, m, ray, inv, w, anc, &pf) == WALK_MISS) w.ndone = 1;
-            return w.ndone && w.lpos >= w.lend && w.nlf >= w.nle ? WALK_MISS : WALK_RUN;
-        }
-#endif
-#if RT_WALK_HOIST == 1
-        // The open leaf's triangles are loaded BEFORE the node operation: while a leaf is open the node
-        // walk only fills the one-leaf buffer (nlf / nle), so the cursor stays as loaded and the slot load
-        // of the pick and the triangle loads are in flight together (one memory latency per step instead
-        // of two in a row). A leaf the node walk opens into a free cursor is tested from the next step:
-        // the same leaves in the same order, the same result.
+        // Hoist 1: the open leaf's triangles (and their ids, RT_LTRI_ID_HOIST) are loaded BEFORE the node
+        // operation: while a leaf is open the node walk only fills the one-leaf buffer (nlf / nle), so the
+        // cursor stays as loaded and the slot load of the pick and the triangle loads are in flight
+        // together (one memory latency per step instead of two in a row). A leaf the node walk opens into
+        // a free cursor is tested from the next step: the same leaves in the same order, the same result.
+        // Hoist 2: triangle tests first, with the next node operation's loads issued before them (the
+        // pick's slot and a pop's box, slot_prefetch). Hoist 0: node operation, then leaf_tris.
         const bool open = w.lpos < w.lend;
         LeafTri tr[kTrisPerStep];
-        if (open) {
+        int32_t tid[kTrisPerStep];
+        if (Hoist != 0 && open) {
 #pragma unroll
-            for (int j = 0; j < kTrisPerStep; ++j) tr[j] = sc.ltris[min(w.lpos + j, w.lend - 1)];
+            for (int j = 0; j < kTrisPerStep; ++j) {
+                tr[j] = sc.ltris[min(w.lpos + j, w.lend - 1)];
+                if (RT_LTRI_ID_HOIST) tid[j] = sc.ltri_id[min(w.lpos + j, w.lend - 1)];
+            }
         }
-#endif
-        if (!w.ndone && w.nlf >= w.nle && walk_node_slots<AS>(sc, m, ray, inv, w, anc) == WALK_MISS) w.ndone = 1;
+        SlotPF pf;
+        pf.kind = 0;
+        if constexpr (Hoist == 2) {
+            if (!w.ndone) slot_prefetch<AS>(sc, w, anc, pf);
+        } else {
+            if (!w.ndone && w.nlf >= w.nle && walk_node_slots<AS>(sc, m, ray, inv, w, anc) == WALK_MISS) w.ndone = 1;
+        }
         RT_DBG_TSTART(t_lt);
-#if RT_WALK_HOIST == 1
-        if (open) {
-            const int st = leaf_tris_loaded(sc, ray, w, tr, t, prim);
-#else
-        if (w.lpos < w.lend) {
-            const int st = leaf_tris(sc, ray, w, t, prim);
-#endif
+        if (Hoist != 0 ? open : w.lpos < w.lend) {
+            const int st = Hoist != 0 ? leaf_tris_loaded(sc, ray, w, tr, t, prim, RT_LTRI_ID_HOIST ? tid : nullptr)
+                                      : leaf_tris(sc, ray, w, t, prim);
             if (st == WALK_HIT) {
                 RT_DBG_TEND(12, t_lt);
                 return WALK_HIT;
@@ -1206,6 +1185,9 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
             }
         }
         RT_DBG_TEND(12, t_lt);
+        if constexpr (Hoist == 2) {
+            if (!w.ndone && w.nlf >= w.nle && walk_node_slots<AS>(sc, m, ray, inv, w, anc, &pf) == WALK_MISS) w.ndone = 1;
+        }
         return w.ndone && w.lpos >= w.lend && w.nlf >= w.nle ? WALK_MISS : WALK_RUN;
     }
     int st = -1;

@@ -251,7 +251,7 @@ RT_DEV bool walk_round(const DevScene& sc, const Park& pk, const bool wk, const 
                 } else {
                     double t;
                     int prim;
-                    const int st = walk_step<S>(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim);
+                    const int st = walk_step<S, 256, C::phong ? 0 : RT_WALK_HOIST>(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim);
                     if (st != WALK_RUN) {
                         if (closest) {
                             if (st == WALK_HIT) {
@@ -406,7 +406,7 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
             if (!fin && r.w.cur >= 0) {
                 double t;
                 int prim;
-                const int st = walk_step<S, kPoolThreads>(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim,
+                const int st = walk_step<S, kPoolThreads, C::phong ? 0 : RT_WALK_HOIST>(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim,
                                             S ? (LdsAncI32*)park_i + kPark2I * kPoolThreads + q : nullptr);
                 if (st != WALK_RUN) {
                     if (closest) {
