@@ -1557,6 +1557,7 @@ RT_DEV HitRec trace_analytic(const DevScene& sc, const Ray& ray, const RayInv& i
         if (i < T->n_sph && sphere_c(T->sph[i], ray, &t)) consider(h, t, T->sph_idx[i], -1);
     }
     for (int i = 0; i < T->n_gen; ++i) {
+        if (!((T->gen_analytic >> i) & 1u)) continue;  // a mesh: analytic_t cannot hit it
         const int idx = T->gen_idx[i];
         const DevObject& o = object_at<C>(sc, idx);
         double t;
@@ -1584,15 +1585,17 @@ RT_DEV void trace_meshes(const DevScene& sc, const Ray& ray, const RayInv& inv, 
 // can meet the box (t <= |o| + 4 S for a box inside [-S, S]^3) all of it moves the ray's points by less
 // than 2^-21 (|o| + S). The box is padded by pad = 2^-16 (max |o_k| + S), 16x that (and 30x the f64
 // test's own 1e-7 S pad), and the interval ends are compared with the same slack.
-RT_DEV bool near_mesh32(const DevMesh& m, const Ray& ray, double tmax) {
+// c: the cull32 box (6 floats, any address space), s: cull32_s.
+template <class CP>
+RT_DEV bool near_cull32(CP c, float s, const Ray& ray, double tmax) {
     const float o[3] = {(float)ray.o.x, (float)ray.o.y, (float)ray.o.z};
     const float d[3] = {(float)ray.d.x, (float)ray.d.y, (float)ray.d.z};
-    const float pad = 0x1p-16f * (fmaxf(fabsf(o[0]), fmaxf(fabsf(o[1]), fabsf(o[2]))) + m.cull32_s);
+    const float pad = 0x1p-16f * (fmaxf(fabsf(o[0]), fmaxf(fabsf(o[1]), fabsf(o[2]))) + s);
     float t0 = 0.0f, t1 = INFINITY;
     bool keep = true;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const float lo = m.cull32[k] - pad, hi = m.cull32[3 + k] + pad;
+        const float lo = c[k] - pad, hi = c[3 + k] + pad;
         const bool tiny = !(fabsf(d[k]) >= 0x1p-60f);  // (nearly) parallel slab (or NaN): origin inside it
         keep &= !tiny || !(o[k] < lo || o[k] > hi);
         const float rc = __builtin_amdgcn_rcpf(d[k]);
@@ -1603,6 +1606,7 @@ RT_DEV bool near_mesh32(const DevMesh& m, const Ray& ray, double tmax) {
     const float tm = (float)tmax;
     return keep && !(t0 > t1 + 0x1p-16f * fabsf(t1) + pad) && !(t0 > tm + 0x1p-16f * tm + pad);
 }
+RT_DEV bool near_mesh32(const DevMesh& m, const Ray& ray, double tmax) { return near_cull32(m.cull32, m.cull32_s, ray, tmax); }
 #ifndef RT_NEAR32
 #define RT_NEAR32 1  // A/B: the meshes' near test in f32 (near_mesh32) or f64 (near_box)
 #endif
@@ -1613,16 +1617,18 @@ RT_DEV uint32_t mesh_near_mask(const DevScene& sc, const Ray& ray, const RayInv&
     CTab* T = tables(sc);
     uint32_t mask = 0;
     for (int i = 0; i < T->n_gen; ++i) {
+#if RT_NEAR32
+        // the slot's mesh and its f32 cull box from the compact table (no object / mesh reads)
+        (void)inv;
+        const int mm = T->gen_mesh[i];
+        if (mm >= 0) mask |= near_cull32(T->gen_cull32[i], T->gen_cull32[i][6], ray, tmax) ? 1u << mm : 0u;
+#else
         const DevObject& o = object_at<C>(sc, T->gen_idx[i]);
         if (o.geom == GEOM_MESH && sc.meshes[o.mesh].n_nodes > 0) {
             const DevMesh& m = sc.meshes[o.mesh];
-#if RT_NEAR32
-            (void)inv;
-            mask |= near_mesh32(m, ray, tmax) ? 1u << o.mesh : 0u;
-#else
             mask |= near_box(m.cull_box, ray, inv, m.cull_pad, tmax) ? 1u << o.mesh : 0u;
-#endif
         }
+#endif
     }
     return mask;
 }
@@ -1651,6 +1657,7 @@ RT_DEV bool visible_analytic(const DevScene& sc, V3 y, const Ray& r, const RayIn
     }
     if (occluded) return false;
     for (int i = 0; i < T->n_gen; ++i) {
+        if (!((T->gen_analytic >> i) & 1u)) continue;  // a mesh: analytic_t cannot hit it
         const DevObject& o = object_at<C>(sc, T->gen_idx[i]);
         double t;
         if (analytic_t(o, r, inv, &t) && !(t + ERR_MARGIN >= dist)) return false;

@@ -157,6 +157,11 @@ struct CompactTab {
     int32_t sph_idx[kMaxSpheres];
     double sph[kMaxSpheres][4];              // centre xyz, r*r
     int32_t gen_idx[kMaxGeneric];            // everything else, through the generic intersector
+    // per gen slot, so the per-ray loops over the gen slots read only this table (scalar loads issued
+    // together) instead of the object and then its mesh (a chain of dependent loads):
+    uint32_t gen_analytic;                   // bit g: slot g is a sphere or plane (analytic_t can hit it)
+    int32_t gen_mesh[kMaxGeneric];           // slot g's mesh when it is a mesh with a non-empty octree, else -1
+    float gen_cull32[kMaxGeneric][8];        // that mesh's cull32[0..5] and cull32_s (near_mesh32's operands)
 };
 typedef const __attribute__((address_space(4))) CompactTab CTab;
 

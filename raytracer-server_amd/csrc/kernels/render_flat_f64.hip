@@ -403,11 +403,10 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
         if (go) {
             CTab* T = tables(sc);
             for (int g = 0; g < T->n_gen; ++g) {  // Scene::trace_ray's loop over the meshes (ties: lower index)
-                const int idx = T->gen_idx[g];
-                const DevObject& o = object_at<C>(sc, idx);
-                if (o.geom == GEOM_MESH && ((qmask >> o.mesh) & 1u)) {
-                    const int p = s_rp[o.mesh * kBlk + tid];
-                    if (p >= 0) consider(h, s_rt[o.mesh * kBlk + tid], idx, p);
+                const int mm = T->gen_mesh[g];   // the slot's mesh (CompactTab; -1: not a mesh, or empty)
+                if (mm >= 0 && ((qmask >> mm) & 1u)) {
+                    const int p = s_rp[mm * kBlk + tid];
+                    if (p >= 0) consider(h, s_rt[mm * kBlk + tid], T->gen_idx[g], p);
                 }
             }
             nverts += h.obj >= 0;
@@ -642,11 +641,11 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
             } else if (traced) {
                 CTab* T = tables(sc);
                 for (int g = 0; g < T->n_gen; ++g) {  // Scene::trace_ray's loop over the meshes (ties: lower index)
-                    const int idx = T->gen_idx[g];
-                    const DevObject& o = object_at<C>(sc, idx);
-                    if (o.geom == GEOM_MESH && ((qmask >> o.mesh) & 1u)) {
-                        const int p = s_rp[o.mesh * kBlk + tid];
-                        if (p != 0xFF) consider(h, s_rt[o.mesh * kBlk + tid], idx, sc.meshes[o.mesh].tri_base + p);
+                    // the slot's mesh from the compact table (-1: not a mesh, or an empty one, which has no hit)
+                    const int mm = T->gen_mesh[g];
+                    if (mm >= 0 && ((qmask >> mm) & 1u)) {
+                        const int p = s_rp[mm * kBlk + tid];
+                        if (p != 0xFF) consider(h, s_rt[mm * kBlk + tid], T->gen_idx[g], sc.meshes[mm].tri_base + p);
                     }
                 }
                 nverts += h.obj >= 0;

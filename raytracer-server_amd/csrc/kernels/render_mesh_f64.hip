@@ -27,10 +27,11 @@ typedef __attribute__((address_space(3))) uint64_t LdsU64;
 template <class C, bool S>
 RT_DEV bool next_mesh_walk(const DevScene& sc, const Ray& r, const RayInv& inv, double tmax, int& g, int& mi,
                            OctWalk& w) {
-    for (++g; g < tables(sc)->n_gen; ++g) {
-        const DevObject& o = object_at<C>(sc, tables(sc)->gen_idx[g]);
-        if (o.geom == GEOM_MESH && walk_begin<S>(sc, sc.meshes[o.mesh], r, inv, tmax, w)) {
-            mi = o.mesh;
+    CTab* T = tables(sc);
+    for (++g; g < T->n_gen; ++g) {
+        const int mm = T->gen_mesh[g];  // the slot's mesh (non-empty octree), or -1 (CompactTab)
+        if (mm >= 0 && walk_begin<S>(sc, sc.meshes[mm], r, inv, tmax, w)) {
+            mi = mm;
             return true;
         }
     }
@@ -41,10 +42,13 @@ RT_DEV bool next_mesh_walk(const DevScene& sc, const Ray& r, const RayInv& inv, 
 template <class C, bool S>
 RT_DEV bool next_mesh_walk_near(const DevScene& sc, const Ray& r, const RayInv& inv, double tmax, int& g, int& mi,
                                 OctWalk& w, uint32_t near) {
-    for (++g; g < tables(sc)->n_gen; ++g) {
-        const DevObject& o = object_at<C>(sc, tables(sc)->gen_idx[g]);
-        if (o.geom == GEOM_MESH && ((near >> o.mesh) & 1u) && walk_begin<S>(sc, sc.meshes[o.mesh], r, inv, tmax, w, false)) {
-            mi = o.mesh;
+    CTab* T = tables(sc);
+    for (++g; g < T->n_gen; ++g) {
+        // the slot's mesh from the compact table (one load, not the object and then its mesh); `near`
+        // only has bits of meshes with a non-empty octree, like gen_mesh
+        const int mm = T->gen_mesh[g];
+        if (mm >= 0 && ((near >> mm) & 1u) && walk_begin<S>(sc, sc.meshes[mm], r, inv, tmax, w, false)) {
+            mi = mm;
             return true;
         }
     }

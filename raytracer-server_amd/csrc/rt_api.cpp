@@ -569,6 +569,19 @@ void fill_compact(const Packed& p, rt::CompactTab* ds, int32_t* compact) {
     ds->last_mesh_g = -1;
     for (int g = 0; g < ds->n_gen; ++g)
         if (p.objects[ds->gen_idx[g]].geom == rt::GEOM_MESH) ds->last_mesh_g = g;
+    ds->gen_analytic = 0;
+    for (int g = 0; g < rt::kMaxGeneric; ++g) {
+        ds->gen_mesh[g] = -1;
+        if (g >= ds->n_gen) continue;
+        const rt::DevObject& o = p.objects[ds->gen_idx[g]];
+        if (o.geom == rt::GEOM_SPHERE || o.geom == rt::GEOM_PLANE) ds->gen_analytic |= 1u << g;
+        if (o.geom == rt::GEOM_MESH && o.mesh >= 0 && o.mesh < (int)p.meshes.size() && p.meshes[o.mesh].n_nodes > 0) {
+            const rt::DevMesh& m = p.meshes[o.mesh];
+            ds->gen_mesh[g] = o.mesh;
+            for (int k = 0; k < 6; ++k) ds->gen_cull32[g][k] = m.cull32[k];
+            ds->gen_cull32[g][6] = m.cull32_s;
+        }
+    }
 }
 
 // f32 perf-mode tables (scene_layout.h: Obj32 / Bvh32 / Tri32). BVH boxes are rounded outward and
