@@ -242,16 +242,21 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
             if constexpr (C::mesh && C::compact) {
                 if (defer) {
                     // mutually_visible (scene.rs:258-270) split: analytic objects now, meshes deferred
-                    const RayInv inv = make_inv(sr.d);
-                    vis = visible_analytic<C>(sc, y, sr, inv, dist) ? 1. : 0.;
-                    const uint32_t near = vis > 0. ? mesh_near_mask<C>(sc, sr, inv, dist) : 0u;
+                    // (the reciprocals only where used: the plane tests, f64 near tests, the deferral)
+                    vis = visible_analytic<C>(sc, y, sr, dist) ? 1. : 0.;
+#if RT_NEAR32
+                    const RayInv ninv{};  // near_cull32 takes its own f32 reciprocals
+#else
+                    const RayInv ninv = make_inv(sr.d);
+#endif
+                    const uint32_t near = vis > 0. ? mesh_near_mask<C>(sc, sr, ninv, dist) : 0u;
                     if (near) {
                         defer->pending = true;
                         defer->meshes = near;
                         if constexpr (Sink::lds) {
                             sink.put(sr.o, sr.d, dist);
                         } else {
-                            defer->inv = inv;
+                            defer->inv = make_inv(sr.d);
                             defer->o = sr.o;
                             defer->d = sr.d;
                             defer->dist = dist;

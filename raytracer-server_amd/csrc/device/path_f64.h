@@ -1638,14 +1638,17 @@ RT_DEV bool mesh_candidate(const DevScene& sc, const Ray& ray, const RayInv& inv
 }
 // mutually_visible split: the analytic objects here, the meshes later (mesh_occludes).
 template <class C>
-RT_DEV bool visible_analytic(const DevScene& sc, V3 y, const Ray& r, const RayInv& inv, double dist) {
+RT_DEV bool visible_analytic(const DevScene& sc, V3 y, const Ray& r, double dist) {
     CTab* T = tables(sc);
     const double ERR_MARGIN = 0.001;
     bool occluded = false;
     auto visit = [&](double t, int, int) { occluded |= !(t + ERR_MARGIN >= dist); };
     const bool clear = dist < 1e9 && planes_clear<0>(T, r.o.x, y.x) && planes_clear<1>(T, r.o.y, y.y) &&
                        planes_clear<2>(T, r.o.z, y.z);
+    // the ray reciprocals only where they are used (make_inv's wave vote makes it a convergent call
+    // the compiler cannot sink into these branches itself; its result is the same bits either way)
     if (!clear) {
+        const RayInv inv = make_inv(r.d);
         axis_planes<0>(sc, T, r, inv, visit);
         axis_planes<1>(sc, T, r, inv, visit);
         axis_planes<2>(sc, T, r, inv, visit);
@@ -1656,11 +1659,14 @@ RT_DEV bool visible_analytic(const DevScene& sc, V3 y, const Ray& r, const RayIn
         if (i < T->n_sph && sphere_c(T->sph[i], r, &t)) occluded |= !(t + ERR_MARGIN >= dist);
     }
     if (occluded) return false;
-    for (int i = 0; i < T->n_gen; ++i) {
-        if (!((T->gen_analytic >> i) & 1u)) continue;  // a mesh: analytic_t cannot hit it
-        const DevObject& o = object_at<C>(sc, T->gen_idx[i]);
-        double t;
-        if (analytic_t(o, r, inv, &t) && !(t + ERR_MARGIN >= dist)) return false;
+    if (T->gen_analytic) {
+        const RayInv inv = make_inv(r.d);
+        for (int i = 0; i < T->n_gen; ++i) {
+            if (!((T->gen_analytic >> i) & 1u)) continue;  // a mesh: analytic_t cannot hit it
+            const DevObject& o = object_at<C>(sc, T->gen_idx[i]);
+            double t;
+            if (analytic_t(o, r, inv, &t) && !(t + ERR_MARGIN >= dist)) return false;
+        }
     }
     return true;
 }

@@ -151,7 +151,8 @@ typedef const __attribute__((address_space(4))) DevTri CTri;
 // hit is the first of the two hits that lies in it unless the second is strictly nearer (the leaf
 // lists are in triangle order, so the earlier hit is the lower index: the walk's strict <). Same
 // bits as flat_query_leaves, without its per-leaf best-hit updates (8 leaves x 4 VALU per triangle).
-RT_DEV bool flat_query(const DevScene& sc, int mi, const Ray& ray, const RayInv& inv, double* t_out, int* prim_out) {
+// The ray reciprocals are taken only for lanes whose ray hits a triangle (the leaf boxes' test).
+RT_DEV bool flat_query(const DevScene& sc, int mi, const Ray& ray, double* t_out, int* prim_out) {
     CMesh* M = (CMesh*)(uintptr_t)(sc.meshes + mi);
     const int n = M->n_tris, base = M->tri_base;
     CTri* T = (CTri*)(uintptr_t)(sc.tris + base);
@@ -176,7 +177,7 @@ RT_DEV bool flat_query(const DevScene& sc, int mi, const Ray& ray, const RayInv&
         }
     }
     if (__any(nh > 2)) {
-        if (nh > 2) return flat_query_leaves(sc, sc.meshes[mi], ray, inv, t_out, prim_out);
+        if (nh > 2) return flat_query_leaves(sc, sc.meshes[mi], ray, make_inv(ray.d), t_out, prim_out);
     }
     int win = -1;
     if (M->flat_root_leaf) {
@@ -187,7 +188,7 @@ RT_DEV bool flat_query(const DevScene& sc, int mi, const Ray& ray, const RayInv&
             double rb[6];
 #pragma unroll
             for (int k = 0; k < 6; ++k) rb[k] = M->root_box[k];
-            cand &= octant_mask(rb, rb + 3, ray, inv);  // the children's box_hit, bit i = octant i
+            cand &= octant_mask(rb, rb + 3, ray, make_inv(ray.d));  // the children's box_hit, bit i = octant i
             if (cand) win = first_visited(*M, ray, cand);
         }
     }
@@ -241,10 +242,9 @@ RT_DEV void process_queries(const DevScene& sc, const int32_t* cnt_c, const int3
                 const LdsD* q = kind ? qs : qc;
                 const Ray r{v3(q[who], q[kBlk + who], q[2 * kBlk + who]),
                             v3(q[3 * kBlk + who], q[4 * kBlk + who], q[5 * kBlk + who])};
-                const RayInv inv = make_inv(r.d);
                 double t = 0.0;
                 int prim = -1;
-                const bool hit = flat_query(sc, m, r, inv, &t, &prim);
+                const bool hit = flat_query(sc, m, r, &t, &prim);
                 if (kind == 0) {
                     rt[m * kBlk + who] = t;
                     rp[m * kBlk + who] = hit ? prim : -1;
@@ -270,10 +270,9 @@ RT_DEV void process_queries(const DevScene& sc, const int32_t* cnt_c, const int3
                     const int who = queue[m * kBlk + e];
                     const Ray r{v3(q[who], q[kBlk + who], q[2 * kBlk + who]),
                                 v3(q[3 * kBlk + who], q[4 * kBlk + who], q[5 * kBlk + who])};
-                    const RayInv inv = make_inv(r.d);
                     double t = 0.0;
                     int prim = -1;
-                    const bool hit = flat_query(sc, m, r, inv, &t, &prim);
+                    const bool hit = flat_query(sc, m, r, &t, &prim);
                     if (kind == 0) {
                         rt[m * kBlk + who] = t;
                         rp[m * kBlk + who] = hit ? prim : -1;
@@ -599,10 +598,9 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                     const LdsD* q = kind ? (const LdsD*)s_qds : (const LdsD*)s_qdc;
                     const Ray r{v3(qo[who], qo[kBlk + who], qo[2 * kBlk + who]),
                                 v3(q[who], q[kBlk + who], q[2 * kBlk + who])};
-                    const RayInv inv = make_inv(r.d);
                     double t = 0.0;
                     int prim = -1;
-                    const bool hit = flat_query(sc, m, r, inv, &t, &prim);
+                    const bool hit = flat_query(sc, m, r, &t, &prim);
                     RT_DBG(0);           // diagnostic builds: queries evaluated ...
                     if (hit) RT_DBG(1);  // ... and those with a triangle hit
                     if (kind == 0) {
