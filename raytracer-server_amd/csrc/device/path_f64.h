@@ -566,11 +566,11 @@ __shared__ unsigned long long s_dbg_reg[32];
 // g_dbg_time at the kernel's end; blocks of up to 512 threads (8 waves).
 #if RT_DEBUG_TIMERS
 __device__ unsigned long long g_dbg_time[16];
-__shared__ unsigned long long s_dbg_time[8 * 16];
+__shared__ unsigned long long s_dbg_time[16 * 16];
 #define RT_DBG_TSTART(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define RT_DBG_TEND(i, v) do { const uint64_t d_ = __builtin_amdgcn_s_memtime() - (v); const unsigned long long m_ = __ballot(1); if (__lane_id() == __ffsll((long long)m_) - 1) atomicAdd(&s_dbg_time[(threadIdx.x >> 6) * 16 + (i)], (unsigned long long)d_); } while (0)
-#define RT_DBG_TIMERS_INIT() do { for (unsigned i_ = threadIdx.x; i_ < 8 * 16; i_ += blockDim.x) s_dbg_time[i_] = 0; } while (0)
-#define RT_DBG_TIMERS_FLUSH() do { for (unsigned i_ = threadIdx.x; i_ < 8 * 16; i_ += blockDim.x) atomicAdd(&g_dbg_time[i_ & 15], s_dbg_time[i_]); } while (0)
+#define RT_DBG_TIMERS_INIT() do { for (unsigned i_ = threadIdx.x; i_ < 16 * 16; i_ += blockDim.x) s_dbg_time[i_] = 0; } while (0)
+#define RT_DBG_TIMERS_FLUSH() do { for (unsigned i_ = threadIdx.x; i_ < 16 * 16; i_ += blockDim.x) atomicAdd(&g_dbg_time[i_ & 15], s_dbg_time[i_]); } while (0)
 #else
 #define RT_DBG_TSTART(v) ((void)0)
 #define RT_DBG_TEND(i, v) ((void)0)

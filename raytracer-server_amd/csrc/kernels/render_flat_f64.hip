@@ -501,16 +501,23 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
 // that ray's closest-hit queries. A path thus waits only for its own queries, queries are evaluated
 // in fuller chunks, and no wave waits at a barrier for another wave's chunk (the block-synchronous
 // kernel spent 24% of its wave time in barrier waits, 2 waves of 4 working in phase P).
-constexpr int kFpRing = 512;  // per mesh: at most 256 closest-hit + 256 shadow queries queued at once
+#ifndef RT_FPOOL_BLOCK
+#define RT_FPOOL_BLOCK 768  // threads per query-pool block of the no-mirror instance: one block per CU (12 waves
+                            // share one query queue per mesh), or 256 (three blocks per CU, A/B)
+#endif
 #ifndef RT_FPOOL_SINK
 #define RT_FPOOL_SINK 1  // A/B: shade_vertex writes the shadow query's ray into the LDS columns (LdsQuerySink)
 #endif
 
-template <int F, int W>
-__global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g, RenderArgs a_g, double* __restrict__ sub_buf,
+template <int F, int W, int B = kBlk>
+__global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, RenderArgs a_g, double* __restrict__ sub_buf,
                                                                  uint32_t* next_sub, long nsub, int pool_min, int refill) {
     using C = Cfg<F | kCfgLdsObj>;  // the object table in LDS (path_f64.h rt_lds_objects)
     static_assert(C::mesh && C::compact && !C::bvh, "flat-mesh kernel: compact scenes, octree meshes");
+    static_assert(B % 64 == 0 && B <= 1024, "whole waves (path_f64.h: the diagnostic builds' per-wave LDS)");
+    static_assert(C::nospec || B == 256, "LdsCold's columns have a stride of 256");
+    // per mesh: at most B closest-hit + B shadow queries queued at once (a power of two)
+    constexpr int kRing = B <= 256 ? 512 : B <= 512 ? 1024 : 2048;
 #if RT_KARG_VIEW
     const DevScene& sc = karg_scene();  // the arguments read in place (megakernel_common.h)
     const RenderArgs& a = karg_render_args();
@@ -528,29 +535,29 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
     // t, and the hit triangle as its index within the mesh (flat meshes hold <= kFlatMaxTris). The
     // mirror-bounce state (o, pre-bounce throughput) lives in LDS as in k_megakernel_f64 (LdsCold):
     // 12 VGPRs less at 3 waves/SIMD.
-    __shared__ double s_acc[3 * kBlk];
-    __shared__ double s_qo[3 * kBlk], s_qdc[3 * kBlk], s_qds[4 * kBlk];
-    __shared__ double s_rt[kFlatMeshes * kBlk];
-    __shared__ uint8_t s_rp[kFlatMeshes * kBlk];
-    __shared__ uint8_t s_ro[kFlatMeshes * kBlk];
+    __shared__ double s_acc[3 * B];
+    __shared__ double s_qo[3 * B], s_qdc[3 * B], s_qds[4 * B];
+    __shared__ double s_rt[kFlatMeshes * B];
+    __shared__ uint8_t s_rp[kFlatMeshes * B];
+    __shared__ uint8_t s_ro[kFlatMeshes * B];
     // Scenes without a mirror object (Cfg::nospec) have no mirror-bounce state: its 12 KB hold a
     // camera-sample buffer instead (as k_megakernel_f64's: the next sample's camera ray and RNG state,
     // computed for many lanes at once in a refill pass rather than by a few lanes per iteration).
-    __shared__ double s_cold[C::nospec ? 1 : 6 * kBlk];
+    __shared__ double s_cold[C::nospec ? 1 : 6 * B];
     using Cold = std::conditional_t<C::nospec, RegCold, LdsCold>;
     Cold cold{};
     if constexpr (!C::nospec) cold = LdsCold{(LdsD*)s_cold + threadIdx.x};
-    __shared__ double s_nbd[C::nospec ? 3 * kBlk : 1];
-    __shared__ uint64_t s_nbr[C::nospec ? 2 * kBlk : 1];
+    __shared__ double s_nbd[C::nospec ? 3 * B : 1];
+    __shared__ uint64_t s_nbr[C::nospec ? 2 * B : 1];
     LdsD* nbd = (LdsD*)s_nbd + (C::nospec ? threadIdx.x : 0);
     __attribute__((address_space(3))) uint64_t* nbr = (__attribute__((address_space(3))) uint64_t*)s_nbr + (C::nospec ? threadIdx.x : 0);
     bool nvalid = false;  // nbd / nbr hold sample s + 1 of subpixel id
-    __shared__ int32_t s_pend[kBlk];
+    __shared__ int32_t s_pend[B];
     // per mesh: queued queries, entry = lane (closest hit) or 256 + lane (shadow)
-    __shared__ int32_t s_ring[kFlatMeshes][kFpRing];
+    __shared__ int32_t s_ring[kFlatMeshes][kRing];
     __shared__ uint32_t s_head[kFlatMeshes], s_tail[kFlatMeshes];
     const int tid = threadIdx.x;
-    for (int i = tid; i < kFlatMeshes * kFpRing; i += kBlk) (&s_ring[0][0])[i] = -1;
+    for (int i = tid; i < kFlatMeshes * kRing; i += B) (&s_ring[0][0])[i] = -1;
     if (tid < kFlatMeshes) {
         s_head[tid] = 0;
         s_tail[tid] = 0;
@@ -568,7 +575,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
     const long t0 = wave_ticket(next_sub, true);
     unit_of(a, t0, id, end, s);
     bool active = t0 < nunits;
-    acc_l[0] = 0.0; acc_l[kBlk] = 0.0; acc_l[2 * kBlk] = 0.0;
+    acc_l[0] = 0.0; acc_l[B] = 0.0; acc_l[2 * B] = 0.0;
     PathState ps;
     bool fresh = true;
     bool traced = false;   // ps.ray has been traced: h is its analytic hit, qmask its closest-hit queries
@@ -587,27 +594,27 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
             // paths wait (also the frame's end: no query waits for a quorum that never comes)
             const int need = __popcll(__ballot(rdy)) >= 16 ? pool_min : 1;
             for (int m = 0; m < nm; ++m) {
-                const LdsQueue Q{s_ring[m], &s_head[m], &s_tail[m], (uint32_t)kFpRing - 1u};
+                const LdsQueue Q{s_ring[m], &s_head[m], &s_tail[m], (uint32_t)kRing - 1u};
                 const int32_t e = queue_take(Q, need);
                 if (!__any(e >= 0)) continue;
                 RT_DBG_WAVE(13, lane_id_is0());
                 RT_DBG_WAVE(12, e >= 0);
                 if (e >= 0) {
-                    const int kind = e >> 8, who = e & (kBlk - 1);
+                    const int kind = e >= B, who = kind ? e - B : e;  // entry = lane, or B + lane (shadow)
                     const LdsD* qo = (const LdsD*)s_qo;
                     const LdsD* q = kind ? (const LdsD*)s_qds : (const LdsD*)s_qdc;
-                    const Ray r{v3(qo[who], qo[kBlk + who], qo[2 * kBlk + who]),
-                                v3(q[who], q[kBlk + who], q[2 * kBlk + who])};
+                    const Ray r{v3(qo[who], qo[B + who], qo[2 * B + who]),
+                                v3(q[who], q[B + who], q[2 * B + who])};
                     double t = 0.0;
                     int prim = -1;
                     const bool hit = flat_query(sc, m, r, &t, &prim);
                     RT_DBG(0);           // diagnostic builds: queries evaluated ...
                     if (hit) RT_DBG(1);  // ... and those with a triangle hit
                     if (kind == 0) {
-                        s_rt[m * kBlk + who] = t;
-                        s_rp[m * kBlk + who] = hit ? (uint8_t)(prim - sc.meshes[m].tri_base) : (uint8_t)0xFF;
+                        s_rt[m * B + who] = t;
+                        s_rp[m * B + who] = hit ? (uint8_t)(prim - sc.meshes[m].tri_base) : (uint8_t)0xFF;
                     } else {
-                        s_ro[m * kBlk + who] = hit && !(t + 0.001 >= q[3 * kBlk + who]) ? 1 : 0;
+                        s_ro[m * B + who] = hit && !(t + 0.001 >= q[3 * B + who]) ? 1 : 0;
                     }
                     const int32_t left = __hip_atomic_fetch_sub(&s_pend[who], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if (RT_QCHECK && left <= 0) RT_QFAIL(2);
@@ -629,7 +636,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
             if (spend) {  // the last vertex's NEE term, unless a mesh blocks its shadow ray (mutually_visible)
                 bool occluded = false;
                 for (int m = 0; m < nm; ++m)
-                    if ((smask >> m) & 1u) occluded |= s_ro[m * kBlk + tid] != 0;
+                    if ((smask >> m) & 1u) occluded |= s_ro[m * B + tid] != 0;
                 if (!occluded) ps.L = ps.L + pc;
                 spend = false;
             }
@@ -642,8 +649,8 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                     // the slot's mesh from the compact table (-1: not a mesh, or an empty one, which has no hit)
                     const int mm = T->gen_mesh[g];
                     if (mm >= 0 && ((qmask >> mm) & 1u)) {
-                        const int p = s_rp[mm * kBlk + tid];
-                        if (p != 0xFF) consider(h, s_rt[mm * kBlk + tid], T->gen_idx[g], sc.meshes[mm].tri_base + p);
+                        const int p = s_rp[mm * B + tid];
+                        if (p != 0xFF) consider(h, s_rt[mm * B + tid], T->gen_idx[g], sc.meshes[mm].tri_base + p);
                     }
                 }
                 nverts += h.obj >= 0;
@@ -651,7 +658,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                 df.pending = false;
 #if RT_FPOOL_SINK
                 // the shadow query's ray goes straight into this lane's query columns (its s_pend read 0)
-                const LdsQuerySink qsink{(LdsD*)s_qo + tid, (LdsD*)s_qds + tid, kBlk};
+                const LdsQuerySink qsink{(LdsD*)s_qo + tid, (LdsD*)s_qds + tid, B};
                 const bool cont = shade_vertex<C, Cold, LdsQuerySink>(sc, a, ps, h, &df, cold, qsink);
 #else
                 const bool cont = shade_vertex<C, Cold>(sc, a, ps, h, &df, cold);
@@ -680,9 +687,9 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
             want_s = near_s;  // shade_vertex's mesh_near_mask of the segment (non-zero: df.pending)
             if (want_s) {
 #if !RT_FPOOL_SINK
-                s_qo[tid] = sr.o.x; s_qo[kBlk + tid] = sr.o.y; s_qo[2 * kBlk + tid] = sr.o.z;
-                s_qds[tid] = sr.d.x; s_qds[kBlk + tid] = sr.d.y; s_qds[2 * kBlk + tid] = sr.d.z;
-                s_qds[3 * kBlk + tid] = dist;
+                s_qo[tid] = sr.o.x; s_qo[B + tid] = sr.o.y; s_qo[2 * B + tid] = sr.o.z;
+                s_qds[tid] = sr.d.x; s_qds[B + tid] = sr.d.y; s_qds[2 * B + tid] = sr.d.z;
+                s_qds[3 * B + tid] = dist;
 #endif
                 spend = true;
                 smask = want_s;
@@ -699,9 +706,9 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
         if (finish) {
             fresh = true;
             if (id < a.n_whole) {
-                V3 acc = v3(acc_l[0], acc_l[kBlk], acc_l[2 * kBlk]);
+                V3 acc = v3(acc_l[0], acc_l[B], acc_l[2 * B]);
                 acc = acc + ps.L * a.inv_n;  // server.rs:357-358
-                acc_l[0] = acc.x; acc_l[kBlk] = acc.y; acc_l[2 * kBlk] = acc.z;
+                acc_l[0] = acc.x; acc_l[B] = acc.y; acc_l[2 * B] = acc.z;
                 if (++s == a.n_samples) {
                     double* o = sub_buf + (size_t)id * 3;
                     o[0] = acc.x;
@@ -709,7 +716,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
                     o[2] = acc.z;
                     if (++id < end) {  // the next subpixel of the run, no ticket
                         s = 0;
-                        acc_l[0] = 0.0; acc_l[kBlk] = 0.0; acc_l[2 * kBlk] = 0.0;
+                        acc_l[0] = 0.0; acc_l[B] = 0.0; acc_l[2 * B] = 0.0;
                         nvalid = false;
                     } else {
                         done = true;
@@ -731,7 +738,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
         if (done) {
             unit_of(a, nt, id, end, s);
             active = !stop && nt < nunits;
-            acc_l[0] = 0.0; acc_l[kBlk] = 0.0; acc_l[2 * kBlk] = 0.0;
+            acc_l[0] = 0.0; acc_l[B] = 0.0; acc_l[2 * B] = 0.0;
             fresh = true;
             nvalid = false;
         }
@@ -742,8 +749,8 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
             if (refill > 0 && __popcll(__ballot(need)) >= refill) {
                 if (need) {
                     const CameraSample nb = camera_sample(sc, a, subpixel_of(a, id), s + 1);
-                    nbd[0] = nb.d.x; nbd[kBlk] = nb.d.y; nbd[2 * kBlk] = nb.d.z;
-                    nbr[0] = nb.r0; nbr[kBlk] = nb.r1;
+                    nbd[0] = nb.d.x; nbd[B] = nb.d.y; nbd[2 * B] = nb.d.z;
+                    nbr[0] = nb.r0; nbr[B] = nb.r1;
                     nvalid = true;
                 }
             }
@@ -753,7 +760,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
         uint32_t want_c = 0;
         if (tr) {
             if (fresh) {
-                if (C::nospec && nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[kBlk], nbd[2 * kBlk]), nbr[0], nbr[kBlk]}, ps);
+                if (C::nospec && nvalid) begin_path(sc, CameraSample{v3(nbd[0], nbd[B], nbd[2 * B]), nbr[0], nbr[B]}, ps);
                 else begin_sample(sc, a, subpixel_of(a, id), s, ps);
                 nvalid = false;
                 fresh = false;
@@ -770,8 +777,8 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
 #endif
             }
             if (want_c) {
-                s_qo[tid] = ps.ray.o.x; s_qo[kBlk + tid] = ps.ray.o.y; s_qo[2 * kBlk + tid] = ps.ray.o.z;
-                s_qdc[tid] = ps.ray.d.x; s_qdc[kBlk + tid] = ps.ray.d.y; s_qdc[2 * kBlk + tid] = ps.ray.d.z;
+                s_qo[tid] = ps.ray.o.x; s_qo[B + tid] = ps.ray.o.y; s_qo[2 * B + tid] = ps.ray.o.z;
+                s_qdc[tid] = ps.ray.d.x; s_qdc[B + tid] = ps.ray.d.y; s_qdc[2 * B + tid] = ps.ray.d.z;
             }
             qmask = want_c;
             traced = true;
@@ -781,8 +788,8 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
             RT_QFAIL(3);
         if (want_s | want_c) s_pend[tid] = __popc(want_s) + __popc(want_c);
         for (int m = 0; m < nm; ++m) {
-            const LdsQueue Q{s_ring[m], &s_head[m], &s_tail[m], (uint32_t)kFpRing - 1u};
-            queue_put(Q, (want_s >> m) & 1u, kBlk + tid);
+            const LdsQueue Q{s_ring[m], &s_head[m], &s_tail[m], (uint32_t)kRing - 1u};
+            queue_put(Q, (want_s >> m) & 1u, B + tid);
             queue_put(Q, (want_c >> m) & 1u, tid);
         }
         RT_DBG_TEND(3, t_b);
@@ -791,12 +798,12 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_fpool_f64(DevScene sc_g,
     RT_DBG_TFLUSH();
 }
 
-template <int F, int W>
+template <int F, int W, int B = kBlk>
 static void launch_fpool(const DevScene& sc, RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
                          double* tail_buf, size_t tail_cap, int pool_min, int refill, hipStream_t st) {
-    const long blocks = resident_blocks(k_megakernel_fpool_f64<F, W>, (nsub + kBlk - 1) / kBlk);
-    plan_tail(a, nsub, blocks * kBlk, tail_buf, tail_cap);
-    hipLaunchKernelGGL((k_megakernel_fpool_f64<F, W>), dim3((unsigned)blocks), dim3(kBlk), 0, st, sc, a, sub_buf,
+    const long blocks = resident_blocks(k_megakernel_fpool_f64<F, W, B>, (nsub + B - 1) / B, B);
+    plan_tail(a, nsub, blocks * B, tail_buf, tail_cap);
+    hipLaunchKernelGGL((k_megakernel_fpool_f64<F, W, B>), dim3((unsigned)blocks), dim3(B), 0, st, sc, a, sub_buf,
                        next_sub, nsub, pool_min, refill);
 }
 
@@ -834,8 +841,8 @@ hipError_t launch_megakernel_flat_f64(const DevScene& sc, const RenderArgs& a_in
         break;
     if (fpool && nospec && (a.features & 32) && !(a.features & 2)) {  // no mirror, no Phong object
         switch (a.features & 15) {
-            case 9: launch_fpool<9 | 32, 3>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); break;
-            case 13: launch_fpool<13 | 32, 3>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); break;
+            case 9: launch_fpool<9 | 32, 3, RT_FPOOL_BLOCK>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); break;
+            case 13: launch_fpool<13 | 32, 3, RT_FPOOL_BLOCK>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); break;
             default: return hipErrorInvalidValue;
         }
     } else {
