@@ -856,17 +856,6 @@ constexpr int kSlotAncLevels = 9;
 #ifndef RT_LTRI_ID_HOIST
 #define RT_LTRI_ID_HOIST 1  // the hoisted triangle loads also load the triangles' ids (leaf_tris_loaded: unicorn +1.5%, r04o), or not (0)
 #endif
-#ifndef RT_SLOT_XPF
-#define RT_SLOT_XPF 0  // A/B: the walk pool fetches the next pick's two slots at the end of a step (SlotXPF)
-#endif
-// The next pick's two candidate slots, fetched at the end of the step before it (while that step's
-// triangles are tested): valid while the walk is still at (cur, pm), i.e. the next node operation
-// picks there; pm = 0 marks no fetch.
-struct SlotXPF {
-    int4 k1, k2;
-    int32_t cur;
-    uint32_t pm;
-};
 #ifndef RT_SLOT_PAIR
 #define RT_SLOT_PAIR 1  // a pick loads the slots of the next two candidates together (1: unicorn +0.7%, r04j) or one by one (0)
 #endif  // the deepest parents sit at depth 8 (MAX_DEPTH 10, root depth 1)
@@ -915,7 +904,7 @@ RT_DEV void slot_prefetch(const DevScene& sc, const OctWalk& w, const LdsAncI32*
 }
 template <int AS = 256>  // `anc`'s stride (the block's threads)
 RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w,
-                           LdsAncI32* anc = nullptr, const SlotPF* pf = nullptr, const SlotXPF* xpf = nullptr) {
+                           LdsAncI32* anc = nullptr, const SlotPF* pf = nullptr) {
     RT_DBG_TSTART(t_pop);
     uint32_t exist = 0;  // a node to enter: its existence mask (the root at a walk's start, or a descent)
     if (w.enter) {
@@ -987,9 +976,8 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
         const uint32_t pm1 = w.pm & (w.pm - 1u);
         const uint32_t oi1 = (w.order >> (4 * __builtin_ctz(w.pm))) & 0xF;
         const uint32_t oi2 = pm1 ? (w.order >> (4 * __builtin_ctz(pm1))) & 0xF : oi1;
-        const bool xv = xpf && xpf->pm != 0 && xpf->cur == w.cur && xpf->pm == w.pm;
-        const int4 ks1 = xv ? xpf->k1 : kid_slot(sc, w.cur, oi1);
-        const int4 ks2 = xv ? xpf->k2 : kid_slot(sc, w.cur, oi2);
+        const int4 ks1 = kid_slot(sc, w.cur, oi1);
+        const int4 ks2 = kid_slot(sc, w.cur, oi2);
         w.pm = pm1;
         oi = oi1;
         if (!RT_SLOT_CULL || kid_tight_hit(m, ks1, ray, inv)) {
@@ -1149,7 +1137,7 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
 // the hoisted triangles' registers would spill.
 template <bool Slots = (RT_WALK_TIGHT != 0), int AS = 256, int Hoist = RT_WALK_HOIST>
 RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w, double* t,
-                     int* prim, LdsAncI32* anc = nullptr, SlotXPF* xpf = nullptr) {
+                     int* prim, LdsAncI32* anc = nullptr) {
     RT_DBG(5);
     if constexpr (Slots) {
         // The node walk and the triangle tests run in the same step, one leaf apart: the node walk
@@ -1179,23 +1167,7 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         if constexpr (Hoist == 2) {
             if (!w.ndone) slot_prefetch<AS>(sc, w, anc, pf);
         } else {
-            if (!w.ndone && w.nlf >= w.nle && walk_node_slots<AS>(sc, m, ray, inv, w, anc, nullptr, xpf) == WALK_MISS) w.ndone = 1;
-            if (xpf) {
-                // the next pick's slots, in flight during this step's triangle tests
-                if (!w.ndone && !w.enter && w.pm != 0) {
-                    const uint32_t pm1 = w.pm & (w.pm - 1u);
-                    const uint32_t oi1 = (w.order >> (4 * __builtin_ctz(w.pm))) & 0xF;
-                    const uint32_t oi2 = pm1 ? (w.order >> (4 * __builtin_ctz(pm1))) & 0xF : oi1;
-                    if (!(xpf->pm != 0 && xpf->cur == w.cur && xpf->pm == w.pm)) {
-                        xpf->k1 = kid_slot(sc, w.cur, oi1);
-                        xpf->k2 = kid_slot(sc, w.cur, oi2);
-                        xpf->cur = w.cur;
-                        xpf->pm = w.pm;
-                    }
-                } else {
-                    xpf->pm = 0;
-                }
-            }
+            if (!w.ndone && w.nlf >= w.nle && walk_node_slots<AS>(sc, m, ray, inv, w, anc) == WALK_MISS) w.ndone = 1;
         }
         RT_DBG_TSTART(t_lt);
         if (Hoist != 0 ? open : w.lpos < w.lend) {

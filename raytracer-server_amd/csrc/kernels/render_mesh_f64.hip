@@ -388,8 +388,6 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
     WalkRegs r;
     bool closest = false;
     auto col = [&](int32_t c) { return Park2{park_d + c, park_i + c}; };
-    SlotXPF xp;  // RT_SLOT_XPF: the next pick's slots (reset with each query taken)
-    xp.pm = 0;
     if (q >= 0) {
         park2_load(col(q), r);
         const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -413,8 +411,7 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
                 double t;
                 int prim;
                 const int st = walk_step<S, kPoolThreads, C::phong ? 0 : RT_WALK_HOIST>(sc, sc.meshes[r.mi], r.wr, r.wi, r.w, &t, &prim,
-                                            S ? (LdsAncI32*)park_i + kPark2I * kPoolThreads + q : nullptr,
-                                            (RT_SLOT_XPF && S && !C::phong) ? &xp : nullptr);
+                                            S ? (LdsAncI32*)park_i + kPark2I * kPoolThreads + q : nullptr);
                 if (st != WALK_RUN) {
                     if (closest) {
                         if (st == WALK_HIT) {
@@ -446,7 +443,6 @@ RT_DEV bool pool_round(const DevScene& sc, const WalkPool& wp, LdsDouble* park_d
             const int32_t q2 = queue_take_each(wp.q, q < 0);
             if (q2 >= 0) {
                 q = q2;
-                xp.pm = 0;
                 park2_load(col(q), r);
                 const uint8_t stq = __hip_atomic_load(&wp.status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 closest = stq == POOL_CLOSEST;
