@@ -505,6 +505,9 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
 #define RT_FPOOL_BLOCK 768  // threads per query-pool block of the no-mirror instance: one block per CU (12 waves
                             // share one query queue per mesh), or 256 (three blocks per CU, A/B)
 #endif
+#ifndef RT_FPOOL_READY
+#define RT_FPOOL_READY 16  // a wave with at least this many ready paths waits for chunks of pool_min queries
+#endif
 #ifndef RT_FPOOL_SINK
 #define RT_FPOOL_SINK 1  // A/B: shade_vertex writes the shadow query's ray into the LDS columns (LdsQuerySink)
 #endif
@@ -592,7 +595,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
             const bool rdy = active && __hip_atomic_load(&s_pend[tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
             // full chunks while this wave has paths to go on with; anything queued once most of its
             // paths wait (also the frame's end: no query waits for a quorum that never comes)
-            const int need = __popcll(__ballot(rdy)) >= 16 ? pool_min : 1;
+            const int need = __popcll(__ballot(rdy)) >= RT_FPOOL_READY ? pool_min : 1;
             for (int m = 0; m < nm; ++m) {
                 const LdsQueue Q{s_ring[m], &s_head[m], &s_tail[m], (uint32_t)kRing - 1u};
                 const int32_t e = queue_take(Q, need);
