@@ -597,3 +597,70 @@ def test_slot_walk_exact_on_grazing_rays(rt, oracle, tmp_path, monkeypatch):
     t_o, id_o, p_o, n_o = oracle.OracleScene(path).trace(o, d)
     exact = (id_s == id_o) & (t_s == t_o) & np.all(p_s == p_o, axis=1) & np.all(n_s == n_o, axis=1)
     assert exact.all(), f"{np.count_nonzero(~exact)} of {n} rays differ from the oracle"
+
+
+# Generic (non-axis) planes between the meshes in object order: the compact table's gen slots then mix
+# analytic objects and meshes (CompactTab::gen_analytic / gen_mesh / gen_cull32), which the per-ray loops
+# of both mesh kernels read instead of the objects.
+TILTED_PLANE = """[[objects]]
+brdf = {{ type = "diffuse", kd = [{k}, 0.7, 0.6] }}
+geometry = {{ type = "plane", pos = [0.0, {y}, 0.0], n = [{nx}, 1.0, {nz}] }}
+"""
+GEN_CUBES_SCENE = """
+[camera]
+pos = [50.0, 52.0, 295.6]
+dir = [0.0, -0.042612, -1.0]
+[[objects]]
+brdf = { type = "diffuse", kd = [0.75, 0.25, 0.25] }
+geometry = { type = "plane", pos = [1.0, 0.0, 0.0], n = [-1.0, 0.0, 0.0] }
+[[objects]]
+brdf = { type = "diffuse", kd = [0.25, 0.25, 0.75] }
+geometry = { type = "plane", pos = [99.0, 0.0, 0.0], n = [-1.0, 0.0, 0.0] }
+[[objects]]
+brdf = { type = "diffuse", kd = [0.75, 0.75, 0.75] }
+geometry = { type = "plane", pos = [0.0, 0.0, 0.0], n = [0.0, 0.0, -1.0] }
+""" + TILTED_PLANE.format(k=0.7, y=-2.0, nx=0.05, nz=0.02) + """
+[[objects]]
+brdf = { type = "diffuse", kd = [0.9, 0.9, 0.9] }
+geometry = { type = "cube", pos = [20.5, 8.0, 40.5], size = 22.0 }
+transforms = [ { rotate_y = 0.5 } ]
+""" + TILTED_PLANE.format(k=0.6, y=80.0, nx=-0.03, nz=0.04) + """
+[[objects]]
+brdf = { type = "diffuse", kd = [0.9, 0.9, 0.9] }
+geometry = { type = "cube", pos = [63.0, 6.0, 30.0], size = 20.0 }
+transforms = [ { rotate_y = -0.6 } ]
+[[objects]]
+emitted = [50.0, 50.0, 50.0]
+brdf = { type = "diffuse", kd = [0.0, 0.0, 0.0] }
+geometry = { type = "sphere", pos = [50.0, 70.0, 100.0], r = 4.0 }
+"""
+
+
+def test_generic_planes_between_meshes_parity(rt, oracle, tmp_path):
+    """Tilted planes (the generic intersector) placed before, between and after the meshes in object
+    order, so the gen slots alternate analytic objects and meshes: the deep-octree walk pool (chair.obj)
+    and the flat-mesh query pool (two cubes, the no-mirror 768-thread instance) against the oracle at the
+    1e-9 / RGB8 bounds, megakernel and wavefront."""
+    import os
+    from test_host_prep import EXTRA_ASSET_SCENE, REPO
+
+    d = tmp_path / "gen"
+    d.mkdir()
+    os.symlink(os.path.join(REPO, "scenes", "assets"), d / "assets")
+    chair = EXTRA_ASSET_SCENE.format(asset="chair.obj", scale=30.0, ty=24.5)
+    i = chair.index("[[objects]]\nbrdf = { type = \"diffuse\", kd = [0.8, 0.7, 0.5] }")
+    j = chair.index("[[objects]]\nemitted")
+    walk_text = (chair[:i] + TILTED_PLANE.format(k=0.7, y=-2.0, nx=0.05, nz=0.02) + chair[i:j] +
+                 TILTED_PLANE.format(k=0.6, y=80.0, nx=-0.03, nz=0.04) + chair[j:])
+    cases = {"walk pool": walk_text, "query pool": GEN_CUBES_SCENE}
+    for what, text in cases.items():
+        p = d / (what.replace(" ", "_") + ".toml")
+        p.write_text(text)
+        sc, orc = rt.Scene.from_toml(str(p)), oracle.OracleScene(str(p))
+        w, h, spp = 64, 48, 8
+        rgb_o, sub_o, st_o = orc.render(w, h, spp, SEED)
+        assert rgb_o.mean() > 5
+        for mk in (True, False):
+            rgb_g, sub_g, st = rt.render(sc, w, h, spp, SEED, megakernel=mk, want_sub=True)
+            assert 0.9 * st_o["vertices"] <= st["vertices"] <= st_o["vertices"]
+            _assert_parity(rgb_g, sub_g, rgb_o, sub_o, f"generic planes/{what}/{'mk' if mk else 'wf'}")
