@@ -505,6 +505,9 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
 #define RT_FPOOL_BLOCK 768  // threads per query-pool block of the no-mirror instance: one block per CU (12 waves
                             // share one query queue per mesh), or 256 (three blocks per CU, A/B)
 #endif
+#ifndef RT_FPOOL_PRIO
+#define RT_FPOOL_PRIO 0  // A/B: s_setprio 1 around the query chunks (stage 1)
+#endif
 #ifndef RT_FPOOL_READY
 #define RT_FPOOL_READY 16  // a wave with at least this many ready paths waits for chunks of pool_min queries
 #endif
@@ -591,6 +594,9 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
         RT_DBG_WAVE(8, lane_id_is0());
         RT_DBG_TSTART(t_q);
         // ---------------- (1) queued mesh queries, a chunk per mesh
+#if RT_FPOOL_PRIO
+        __builtin_amdgcn_s_setprio(1);  // A/B: the query chunks at raised issue priority
+#endif
         {
             const bool rdy = active && __hip_atomic_load(&s_pend[tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
             // full chunks while this wave has paths to go on with; anything queued once most of its
@@ -624,6 +630,9 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
                 }
             }
         }
+#if RT_FPOOL_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         RT_DBG_TEND(1, t_q);
         RT_DBG_TSTART(t_v);
         // ---------------- (2) paths whose queries are all answered

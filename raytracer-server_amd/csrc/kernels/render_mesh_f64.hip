@@ -300,6 +300,10 @@ struct WalkPool {
     uint8_t* status;    // LDS [block] per owner column: 0 closest query, 1 shadow query, 2 done
 };
 enum : uint8_t { POOL_CLOSEST = 0, POOL_SHADOW = 1, POOL_DONE = 2 };
+#ifndef RT_POOL_PRIO
+#define RT_POOL_PRIO 1  // the walk round at raised issue priority (s_setprio 1: its dependent loads issue ahead of the
+                        // other wave's shading; unicorn +2.3%, r04an), 0 = none, 2 = the vertex phase raised (-2.1%)
+#endif
 #ifndef RT_POOL_REFILL
 #define RT_POOL_REFILL 32
 #endif
@@ -524,7 +528,13 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
         if constexpr (P) {
             // take queued queries (at least pool_min of them while this wave has paths to shade)
             const int ready = __popcll(__ballot(active && !walking));
+#if RT_POOL_PRIO == 1
+            __builtin_amdgcn_s_setprio(1);  // A/B: the walk round at raised issue priority
+#endif
             took = pool_round<C, S>(sc, wp, (LdsDouble*)s_park_d, (LdsInt*)s_park_i, ready ? pool_min : 1, ksteps);
+#if RT_POOL_PRIO == 1
+            __builtin_amdgcn_s_setprio(0);
+#endif
             if (!took && !ready) {
                 __builtin_amdgcn_s_sleep(2);  // every path of this wave waits on walks other waves hold
             }
@@ -539,6 +549,9 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
         const bool was_walking = walking;
         // pool: after a walk round, shade only once pool_vmin paths are ready (denser vertex phases)
         const bool vphase = !P || !took || __popcll(__ballot(active && !walking)) >= pool_vmin;
+#if RT_POOL_PRIO == 2
+        __builtin_amdgcn_s_setprio(1);  // A/B: the vertex phase at raised issue priority (lowered at the iteration's end)
+#endif
         RT_DBG_WAVE(9, vphase && active && !walking);
         if constexpr (P) {
           // Pool kernel: per iteration a ready path first shades the hit it holds (the closest walk's
@@ -760,6 +773,9 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
         }
         RT_DBG_TEND(4, t_bk);
         RT_DBG_TEND(0, t_it);
+#if RT_POOL_PRIO == 2
+        __builtin_amdgcn_s_setprio(0);
+#endif
     }
     flush_count(a.counters, nverts);
     RT_DBG_TFLUSH();
