@@ -506,7 +506,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
                             // share one query queue per mesh), or 256 (three blocks per CU, A/B)
 #endif
 #ifndef RT_FPOOL_PRIO
-#define RT_FPOOL_PRIO 0  // A/B: s_setprio 1 around the query chunks (stage 1)
+#define RT_FPOOL_PRIO 1  // the query chunks (stage 1) at raised issue priority (s_setprio 1: cubes +1.3%, r04ao), or not (0)
 #endif
 #ifndef RT_FPOOL_READY
 #define RT_FPOOL_READY 16  // a wave with at least this many ready paths waits for chunks of pool_min queries
