@@ -11,8 +11,8 @@ fixed: scaling = "strong". Rank 0 prints one JSON line.
 
 roofline (dominant kernel = the render megakernel; kernel_ms = its average device time per launch,
 HIP events recorded on the stream the kernel runs on):
-  * bound "valu_issue_f64" (what limits the megakernel, detailed in `compute` below); achieved / peak /
-    frac keep SURVEY §8(d)'s algorithmic bytes, the figure §8(d) names for roofline.achieved:
+  * bound "hbm": achieved / peak / frac are SURVEY §8(d)'s HBM roofline model, the figure §8(d) names
+    for roofline.achieved (what limits the megakernel itself is in `binds` and `compute` below):
     88 B per camera sample + 280 B per path vertex (the canonical f32 SoA wavefront's state traffic;
     vertices = this run's device counter) over kernel_ms; peak 8.0 TB/s; frac = achieved / peak.
     The megakernel does not stream that state (a path lives in registers), so this is the rate the
@@ -333,7 +333,7 @@ def main():
                                      "meaningful)" if pinned not in (None, "") else "rank -> LOCAL_RANK",
                        "vertices": total_vertices,
                        "vertices_per_sample": round(total_vertices / n_samples, 4)},
-            "roofline": {"bound": "valu_issue_f64" if args.mode == "megakernel" else "hbm",
+            "roofline": {"bound": "hbm",  # achieved / peak / frac below: the HBM model (binds: the real limit)
                          "achieved": round(model_gbs, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(model_gbs / HBM_PEAK_GBS, 4),

@@ -14,6 +14,13 @@ extern "C" {
 int rt_selftest_arith_n(long n, unsigned long long seed, unsigned long long* out, int n_out);
 /* The original entry point: out[0] reciprocal and out[1] quotient mismatches only. */
 int rt_selftest_arith(long n, unsigned long long seed, unsigned long long out[2]);
+/* Device round trips of the pointers every trace call rebuilds (no dereference: any 64-bit pattern is
+ * safe): for each of the n addresses p = ptrs[i], a kernel launched with DevScene.ctab = p,
+ * DevScene.node_slot = p + 16 and RenderArgs.tail_buf = p + 32 as its first two (kernarg) arguments
+ * writes out[6i + k]: k = 0 tables() through the kernarg view, 1 tables() of the by-value argument,
+ * 2 the round-4 sign-extending form (wrong whenever bit 31 of p is set: kept to show the check catches
+ * it), 3 the kernarg view's ctab, 4 its node_slot, 5 the kernarg RenderArgs' tail_buf. Returns 0 or -1. */
+int rt_selftest_tables(const unsigned long long* ptrs, int n, unsigned long long* out);
 /* RT_QCHECK builds (-DRT_QCHECK=1): counters of LDS hand-off protocol violations in the megakernels'
  * work queues since the last call (kernels/megakernel_common.h): [0] ring slot overwritten / bad
  * entry, [1] queue over capacity, [2] outstanding-query count below zero, [3] owner/taker state

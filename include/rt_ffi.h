@@ -155,7 +155,9 @@ int rt_render_device(const rt_scene* scene, const rt_render_params* params, void
  * rows straight into rgb_out: the gather is host-side, no collective. The image is byte-identical to rt_render
  * of the same params (the RNG is keyed by global pixel). cancel is checked between bands and relayed to
  * the running bands' kernels as in rt_render. stats (optional):
- * samples and vertices summed over the bands, device_ms = wall time of the whole call. */
+ * samples and vertices summed over the bands, device_ms = wall time of the whole call.
+ * Errors, checked before any band runs: RT_E_NODEVICE when no HIP device is visible (or the runtime is
+ * absent), RT_E_INVAL for a device ordinal outside [0, device count). */
 int rt_render_multi(const rt_scene* scene, const rt_render_params* params, const int32_t* devices, int32_t n_devices,
                     int32_t band_rows, uint8_t* rgb_out, const volatile int32_t* cancel, rt_render_stats* stats);
 /* The band plan rt_render_multi hands out (no GPU): band b = tile rows [first_row[b], first_row[b] + rows[b]),

@@ -1330,15 +1330,25 @@ RT_DEV void lds_objects_fill(const DevScene& sc) {
 // Per-call view of the compact tables (scene_layout.h: CompactTab). The empty asm makes the pointer
 // opaque, so the scalar loads through it are issued inside each trace call instead of being
 // hoisted to the kernel entry, where the tables would hold ~100 SGPRs across the path loop.
-RT_DEV CTab* tables(const DevScene& sc) {
+// kSext = true is the round-4 first build's reconstruction, in which the builtin's int result of the low
+// word sign-extended into the high word (an illegal address whenever hipMalloc placed the table at a low
+// word with bit 31 set: profiles/r04_ab.log). Only rt_selftest_tables instantiates it, to show that its
+// round-trip check catches that form; every trace call uses kSext = false.
+template <bool kSext = false>
+RT_DEV CTab* tables_form(const DevScene& sc) {
     uint64_t p = (uint64_t)(uintptr_t)sc.ctab;
     // (uniform: readfirstlane keeps the asm's SGPR operand legal where the compiler holds it in a VGPR)
     // (the builtin returns int: through uint32_t, or the low word's sign would fill the high word)
-    p = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)p) |
-        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32)) << 32);
+    if constexpr (kSext)
+        p = (uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)p) |
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32)) << 32);
+    else
+        p = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)p) |
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32)) << 32);
     asm volatile("" : "+s"(p));
     return (CTab*)p;
 }
+RT_DEV CTab* tables(const DevScene& sc) { return tables_form<false>(sc); }
 
 // One object's Geometry::intersect, reporting t (and the triangle for meshes).
 template <class C>

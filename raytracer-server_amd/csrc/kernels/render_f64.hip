@@ -389,6 +389,43 @@ extern "C" int rt_selftest_arith(long n, unsigned long long seed, unsigned long 
     return rt_selftest_arith_n(n, seed, out, 2);
 }
 
+// Pointer round trips of the per-call views every trace call goes through (scene.rs:272-289 reads the
+// scene's tables): the compact-table pointer rebuilt from two readfirstlane halves (tables()), the scene
+// and render arguments read in place in the kernarg segment (karg_scene / karg_render_args at offsets 0
+// and 248, the megakernels' own parameter order). out[0] tables() through the kernarg view, [1] tables()
+// of the by-value argument, [2] the round-4 sign-extending form (tables_form<true>), [3] the kernarg
+// view's raw ctab, [4] its node_slot, [5] karg_render_args().tail_buf. The pointers are never
+// dereferenced, so fabricated addresses are safe.
+__global__ __launch_bounds__(64) void k_selftest_tables(DevScene sc_g, RenderArgs a_g, unsigned long long* out) {
+    const DevScene& sc = karg_scene();
+    const RenderArgs& a = karg_render_args();
+    const uint64_t v[6] = {(uint64_t)(uintptr_t)tables(sc), (uint64_t)(uintptr_t)tables(sc_g),
+                           (uint64_t)(uintptr_t)tables_form<true>(sc), (uint64_t)(uintptr_t)sc.ctab,
+                           (uint64_t)(uintptr_t)sc.node_slot, (uint64_t)(uintptr_t)a.tail_buf};
+    (void)a_g;
+    if (threadIdx.x < 6) out[threadIdx.x] = v[threadIdx.x];
+}
+
+extern "C" int rt_selftest_tables(const unsigned long long* ptrs, int n, unsigned long long* out) {
+    if (!ptrs || !out || n <= 0) return -1;
+    unsigned long long* d = nullptr;
+    if (hipMalloc(&d, 6 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    int rc = 0;
+    for (int i = 0; i < n && !rc; ++i) {
+        DevScene sc{};
+        RenderArgs a{};
+        sc.ctab = (const CompactTab*)(uintptr_t)ptrs[i];
+        sc.node_slot = (const KidSlot*)(uintptr_t)(ptrs[i] + 16);
+        a.tail_buf = (double*)(uintptr_t)(ptrs[i] + 32);
+        hipLaunchKernelGGL(k_selftest_tables, dim3(1), dim3(64), 0, 0, sc, a, d);
+        if (hipGetLastError() != hipSuccess || hipMemcpy(out + 6 * (size_t)i, d, 6 * sizeof(unsigned long long),
+                                                         hipMemcpyDeviceToHost) != hipSuccess)
+            rc = -1;
+    }
+    (void)hipFree(d);
+    return rc;
+}
+
 #define RT_DIAG_TU_FN diag_read_main
 #include "diag_tu.h"
 

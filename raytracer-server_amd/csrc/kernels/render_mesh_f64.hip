@@ -468,6 +468,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
     using C = Cfg<F | (RT_OPT_LDSOBJ ? kCfgLdsObj : 0)>;
     static_assert(C::mesh && C::compact, "mesh megakernel needs the compact tables");
     static_assert(B % 64 == 0 && B <= 1024, "whole waves, at most 16 (path_f64.h: the diagnostic builds' per-wave LDS)");
+    static_assert(!P || (B & (B - 1)) == 0, "the walk queue's ring (one entry per thread) masks its index with B - 1");
     // object table in LDS, as in k_megakernel_f64; the arguments read in place (megakernel_common.h)
 #if RT_KARG_VIEW
     const DevScene& sc = karg_scene();

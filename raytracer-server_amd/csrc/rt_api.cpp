@@ -257,10 +257,12 @@ int pack_scene(rt_scene* s) {
     Packed& p = s->packed;
     const Scene& sc = s->host;
     bool slots_ok = true;
-    // RT_SLOT_MAX_NODE (tests): a lower node-id limit for the slot tables, down to 0 = none (the node_kids
-    // walk for every scene); the encoding itself holds ids below kSlotMaxNode
+    // RT_TEST_SLOT_MAX_PID (tests only): a lower limit on the parent ordinals (pid, the slot rows a KidSlot
+    // entry can name), down to 0 = no slot tables (the node_kids walk for every scene), standing in for a
+    // mesh whose pids exceed the encoding (kSlotMaxNode); named as a test switch so no stray setting of a
+    // production-sounding variable slows every scene down
     int32_t slot_max = rt::kSlotMaxNode;
-    if (const char* v = std::getenv("RT_SLOT_MAX_NODE")) slot_max = std::max(0, std::min(slot_max, std::atoi(v)));
+    if (const char* v = std::getenv("RT_TEST_SLOT_MAX_PID")) slot_max = std::max(0, std::min(slot_max, std::atoi(v)));
     if (slot_max == 0) slots_ok = false;
     for (const Mesh& m : sc.meshes) {
         rt::DevMesh dm{};
@@ -489,9 +491,10 @@ int pack_scene(rt_scene* s) {
         }
         p.meshes.push_back(dm);
     }
-    if (!slots_ok) {
+    if (!slots_ok) {  // the node_kids walk: no slot rows, and no parent boxes (only the slot walk's pops read them)
         p.slots.clear();
         p.pid_up.clear();
+        p.node_box.clear();
     }
     for (const Object& o : sc.objects) {
         rt::DevObject d{};
@@ -747,7 +750,7 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.ctab32 = (const rt::Compact32*)(b + o_tab32);
         ds.compact = compact;
         ds.node_slot = p.slots.empty() ? nullptr : (const rt::KidSlot*)(b + o_slot);
-        ds.node_box = (const double*)(b + o_nbox);
+        ds.node_box = p.slots.empty() ? nullptr : (const double*)(b + o_nbox);
         ds.pid_up = p.slots.empty() ? nullptr : (const int32_t*)(b + o_pup);
         ds.light = s->host.light;
         ds.light_pdf = 0.0;
@@ -1272,12 +1275,11 @@ int rt_render_multi(const rt_scene* scene, const rt_render_params* p, const int3
     int rc = check_params(p);
     if (rc != RT_OK) return rc;
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess) {
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {  // no GPU or no runtime: not the caller's error
         (void)hipGetLastError();
-        ndev = 0;
+        return fail(RT_E_NODEVICE, "rt_render_multi: no HIP device visible");
     }
-    // an ordinal no visible device has is the caller's error (RT_E_INVAL), checked before anything runs;
-    // with no device at all every ordinal is out of range
+    // an ordinal no visible device has is the caller's error (RT_E_INVAL), checked before anything runs
     for (int32_t i = 0; i < n_devices; ++i)
         if (devices[i] < 0 || devices[i] >= ndev)
             return fail(RT_E_INVAL, "device ordinal " + std::to_string(devices[i]) + " out of range (" +

@@ -110,6 +110,8 @@ def _load():
         L.rt_selftest_arith.argtypes = [ctypes.c_long, ctypes.c_ulonglong, P(ctypes.c_ulonglong)]
     if hasattr(L, "rt_selftest_arith_n"):
         L.rt_selftest_arith_n.argtypes = [ctypes.c_long, ctypes.c_ulonglong, P(ctypes.c_ulonglong), ctypes.c_int]
+    if hasattr(L, "rt_selftest_tables"):
+        L.rt_selftest_tables.argtypes = [P(ctypes.c_ulonglong), ctypes.c_int, P(ctypes.c_ulonglong)]
     if hasattr(L, "rt_debug_qcheck"):
         L.rt_debug_qcheck.argtypes = [P(ctypes.c_ulonglong)]
     if hasattr(L, "rt_debug_counters"):
@@ -355,6 +357,17 @@ def selftest_arith(n=1 << 24, seed=0x5EED):
     out = (ctypes.c_ulonglong * 3)()
     _check(lib.rt_selftest_arith_n(n, seed, out, 3))
     return int(out[0]), int(out[1]), int(out[2])
+
+
+def selftest_tables(ptrs):
+    """Device round trips of the per-call pointer views (include/rt_diag.h rt_selftest_tables): per address
+    p, (tables() via the kernarg view, tables() of the by-value argument, the round-4 sign-extending form,
+    kernarg ctab, kernarg node_slot [= p + 16], kernarg RenderArgs.tail_buf [= p + 32])."""
+    n = len(ptrs)
+    inp = (ctypes.c_ulonglong * n)(*ptrs)
+    out = (ctypes.c_ulonglong * (6 * n))()
+    _check(lib.rt_selftest_tables(inp, n, out))
+    return [tuple(int(out[6 * i + k]) for k in range(6)) for i in range(n)]
 
 
 def debug_qcheck():

@@ -26,8 +26,8 @@ def test_exports_every_declared_symbol(rt):
 def test_exports_diagnostics(rt):
     text = open(os.path.join(REPO, "include", "rt_diag.h")).read()
     names = re.findall(r"^int\s+(rt_[a-z_0-9]+)\s*\(", text, re.M)
-    assert names == ["rt_selftest_arith_n", "rt_selftest_arith", "rt_debug_qcheck", "rt_debug_counters",
-                     "rt_debug_regions"]
+    assert names == ["rt_selftest_arith_n", "rt_selftest_arith", "rt_selftest_tables", "rt_debug_qcheck",
+                     "rt_debug_counters", "rt_debug_regions"]
     for n in names:
         assert hasattr(rt.lib, n), f"missing export {n}"
     assert rt.debug_qcheck() is None  # the product library is built without the protocol checks
@@ -57,8 +57,9 @@ def test_errors_are_codes_not_crashes(rt):
 
 def test_render_multi_rejects_bad_device_ordinals(rt):
     """rt_render_multi checks every device ordinal against the visible HIP devices before it starts
-    a worker: an ordinal no device has (negative, or >= the device count; on a host without a GPU
-    every ordinal) is RT_E_INVAL with a message, never a crash."""
+    a worker: an ordinal no device has (negative, or >= the device count) is RT_E_INVAL with a message,
+    never a crash; on a host without a GPU every call is RT_E_NODEVICE (-6), so a caller can tell
+    'no GPU' from 'bad ordinal'."""
     from conftest import scene_path
 
     sc = rt.Scene.from_toml(scene_path("cornell_box"))
@@ -67,18 +68,21 @@ def test_render_multi_rejects_bad_device_ordinals(rt):
     n = rt.lib.rt_device_count()
     for bad in (-1, n, n + 7, 1 << 30):
         devs = (ctypes.c_int32 * 2)(0, bad)
-        assert rt.lib.rt_render_multi(sc.handle, ctypes.byref(p), devs, 2, 0, out, None, None) == -1
-        assert b"out of range" in rt.lib.rt_last_error()
+        rc = rt.lib.rt_render_multi(sc.handle, ctypes.byref(p), devs, 2, 0, out, None, None)
+        if n == 0:
+            assert rc == -6 and b"no HIP device" in rt.lib.rt_last_error()
+        else:
+            assert rc == -1 and b"out of range" in rt.lib.rt_last_error()
 
 
 def test_scene_without_slot_tables_still_loads(rt, monkeypatch):
     """An octree whose node ids exceed the child-slot encoding loads without its slot tables (rt_scene_info
-    [11] = 0) instead of failing; RT_SLOT_MAX_NODE lowers the limit to stand in for a 2^23-node mesh.
+    [11] = 0) instead of failing; RT_TEST_SLOT_MAX_PID lowers the parent-ordinal limit to stand in for a mesh beyond the encoding.
     (The GPU test test_walk_culls_do_not_change_frames renders such a scene.)"""
     from conftest import scene_path
 
     assert rt.Scene.from_toml(scene_path("flying_unicorn")).info()["slot_tables"] == 1
-    monkeypatch.setenv("RT_SLOT_MAX_NODE", "1000")
+    monkeypatch.setenv("RT_TEST_SLOT_MAX_PID", "1000")
     info = rt.Scene.from_toml(scene_path("flying_unicorn")).info()
     assert info["nodes"] == 47183 and info["slot_tables"] == 0
 

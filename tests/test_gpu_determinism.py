@@ -144,7 +144,7 @@ _cull_frames = {}
 
 
 def _cull_run(lib=None, env=None):
-    e = {k: v for k, v in os.environ.items() if k not in ("RT_SLOT_MAX_NODE", "RT_AMD_LIB")}
+    e = {k: v for k, v in os.environ.items() if k not in ("RT_TEST_SLOT_MAX_PID", "RT_AMD_LIB")}
     e.update(RT_REPO=REPO, **(env or {}))
     if lib:
         e["RT_AMD_LIB"] = lib
@@ -160,14 +160,14 @@ def test_walk_culls_do_not_change_frames(variant):
       walkref: the octree walked in the reference's visiting order with no subtree-bounds culls
                (-DRT_WALK_TIGHT=0, lib/variants/walkref.so: node_kids walks);
       near64:  the per-mesh near tests in f64 (near_box) instead of f32 (near_mesh32), -DRT_NEAR32=0;
-      noslots: the default library on a scene loaded without its slot tables (RT_SLOT_MAX_NODE=0, the
+      noslots: the default library on a scene loaded without its slot tables (RT_TEST_SLOT_MAX_PID=0, the
                path a 2^23-node octree takes: the pool kernel's node_kids instance)."""
     if "default" not in _cull_frames:
         _cull_frames["default"] = _cull_run()
     base = _cull_frames["default"]
     assert base["cubes/slots"] == 1 and base["flying_unicorn/slots"] == 1
     if variant == "noslots":
-        got = _cull_run(env={"RT_SLOT_MAX_NODE": "0"})
+        got = _cull_run(env={"RT_TEST_SLOT_MAX_PID": "0"})
         assert got["flying_unicorn/slots"] == 0 and got["cubes/slots"] == 0
     else:
         lib = os.path.join(REPO, "raytracer-server_amd", "lib", "variants", variant + ".so")

@@ -567,13 +567,13 @@ def test_slot_walk_exact_on_grazing_rays(rt, oracle, tmp_path, monkeypatch):
     needle triangles, rays from far origins (1 to 1e5 scene units away) aimed at the triangles'
     vertices and edges — where a ray grazes a subtree's padded bounds — with and without ulp-scale
     offsets. The trace must be bit-identical to the walk without the culls (the same scene loaded
-    without slot tables, RT_SLOT_MAX_NODE=0: the reference's visiting order over node_kids) and to the
+    without slot tables, RT_TEST_SLOT_MAX_PID=0: the reference's visiting order over node_kids) and to the
     oracle's walk (geometry.rs:1237-1295)."""
     path, tri = _skinny_mesh_scene(tmp_path)
     slots = rt.Scene.from_toml(path)
-    monkeypatch.setenv("RT_SLOT_MAX_NODE", "0")
+    monkeypatch.setenv("RT_TEST_SLOT_MAX_PID", "0")
     plain = rt.Scene.from_toml(path)
-    monkeypatch.delenv("RT_SLOT_MAX_NODE")
+    monkeypatch.delenv("RT_TEST_SLOT_MAX_PID")
     assert slots.info()["slot_tables"] == 1 and plain.info()["slot_tables"] == 0
     assert slots.info()["parents"] > 8  # a deep octree
     rng = np.random.default_rng(11)
