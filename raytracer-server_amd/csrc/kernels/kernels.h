@@ -36,6 +36,8 @@ struct RenderArgs {
     int32_t all_flat;              // every mesh is a flat octree (DevMesh::flat) and there are <= 2 of them
 };
 
+// Split-tail scratch bytes per split subpixel (megakernel_common.h plan_tail: the samples after chunk 0).
+size_t tail_scratch_per_subpixel(int n_samples);
 // tail_buf / tail_cap: scratch for the split tail (bytes); the launcher sizes the tail to fit it.
 hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
                                  double* tail_buf, size_t tail_cap, hipStream_t st);

@@ -240,11 +240,10 @@ static inline void plan_units(RenderArgs& a, long lanes) {
 
 static inline void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_buf, size_t tail_cap) {
     static const int tail_env = env_int("RT_MK_TAIL", 1);
-    const size_t per_sub = (size_t)std::max(0, a.n_samples) * 3 * sizeof(double);
-    long n_split = 0;
-    if (tail_env && tail_buf && a.n_samples >= 64 && per_sub > 0)
-        n_split = std::min({lanes, nsub / 2, (long)(tail_cap / per_sub)});
-    a.n_whole = (int32_t)(nsub - n_split);
+    // split subpixels per resident lane, as 1 / RT_MK_TAIL_DIV (2: half a subpixel per lane, i.e. two chunks
+    // per lane at the frame's end, which keeps the end as balanced as one subpixel per lane did while the
+    // scratch traffic halves; 1 = round 4's one subpixel per lane)
+    static const int tail_div = std::max(1, env_int("RT_MK_TAIL_DIV", 2));
     // chunks of 2^chunk_lg samples, about RT_MK_TAIL_CPS (4) per subpixel: every chunk costs a
     // ticket on the one global counter, and short chunks make those atomics the bottleneck of the
     // tail (16 per subpixel measured 11% slower on the whole frame)
@@ -254,9 +253,23 @@ static inline void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_
     a.chunk_lg = 5;
     while ((a.n_samples >> a.chunk_lg) > cps_target) ++a.chunk_lg;
     a.tail_cps = (a.n_samples + (1 << a.chunk_lg) - 1) >> a.chunk_lg;
-    if (a.tail_cps < 2) a.n_whole = (int32_t)nsub;  // nothing to split
+    // chunk 0 of a split subpixel sums in place (tail_stores): scratch only for the samples after it
+    const size_t per_sub = (size_t)std::max(0, a.n_samples - (1 << a.chunk_lg)) * 3 * sizeof(double);
+    long n_split = 0;
+    if (tail_env && tail_buf && a.n_samples >= 64 && a.tail_cps >= 2 && per_sub > 0)
+        n_split = std::min({lanes / tail_div, nsub / 2, (long)(tail_cap / per_sub)});
+    a.n_whole = (int32_t)(nsub - n_split);
     a.tail_buf = tail_buf;
     plan_units(a, lanes);
+}
+// Split tail, per sample of a split subpixel: chunk 0 (samples [0, 2^chunk_lg)) sums its samples in
+// place, acc = acc + L * inv_n from 0 exactly like a whole subpixel, and leaves its partial sum in the
+// subpixel's sub_buf entry; every later chunk stores each sample's radiance for k_tail_sum_f64, which
+// continues the same sequential sum from chunk 0's partial (the same bits as one lane summing all).
+__device__ __forceinline__ bool tail_in_place(const RenderArgs& a, int s) { return (s >> a.chunk_lg) == 0; }
+__device__ __forceinline__ double* tail_slot(const RenderArgs& a, int id, int s) {
+    const int c0 = 1 << a.chunk_lg;
+    return a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)(a.n_samples - c0) + (size_t)(s - c0)) * 3;
 }
 
 // k_tail_sum_f64 for the split tail of a megakernel launch (render_f64.hip)

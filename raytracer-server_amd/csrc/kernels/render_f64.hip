@@ -154,8 +154,20 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
                             done = true;
                         }
                     }
-                } else {  // split tail: the sample's radiance, summed in order by k_tail_sum_f64
-                    double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
+                } else if (tail_in_place(a, s)) {  // split tail, chunk 0: summed in place, its partial sum to sub_buf
+                    V3 acc = v3(acc_l[0], acc_l[256], acc_l[2 * 256]);
+                    acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                    acc_l[0] = acc.x; acc_l[256] = acc.y; acc_l[2 * 256] = acc.z;
+                    done = !unit_has_next(a, id, s);
+                    if (done) {
+                        double* o = sub_buf + (size_t)id * 3;
+                        o[0] = acc.x;
+                        o[1] = acc.y;
+                        o[2] = acc.z;
+                    }
+                    ++s;
+                } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
+                    double* o = tail_slot(a, id, s);
                     o[0] = ps.L.x;
                     o[1] = ps.L.y;
                     o[2] = ps.L.z;
@@ -188,19 +200,20 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
     RT_DBG_TFLUSH();
 }
 
-// Split tail: subpixel n_whole + j's mean from its samples' radiance, summed in sample order
-// exactly as the megakernel's in-register accumulator (acc = acc + L * inv_n, server.rs:357-358).
-// tail_buf is subpixel-major ([j][sample][3]): a chunk's lane writes one contiguous run (the
-// sample-major layout scattered every write over the whole buffer: TLB misses, 2x slower tail).
+// Split tail: subpixel n_whole + j's mean, continuing the sequential sum chunk 0 left in sub_buf (its lane
+// summed samples [0, c0) in place, megakernel_common.h tail_in_place) over the later chunks' stored sample
+// radiance, in sample order, with the same acc + L * inv_n expression as the megakernel's accumulator
+// (server.rs:357-358): the bits of one lane summing every sample. tail_buf is subpixel-major
+// ([j][sample - c0][3]): a chunk's lane writes one contiguous run (the sample-major layout scattered
+// every write over the whole buffer: TLB misses, 2x slower tail).
 __global__ __launch_bounds__(256) void k_tail_sum_f64(RenderArgs a, double* __restrict__ sub_buf, long n_split) {
     const long stride = (long)gridDim.x * blockDim.x;
+    const int c0 = 1 << a.chunk_lg;
     for (long j = (long)blockIdx.x * blockDim.x + threadIdx.x; j < n_split; j += stride) {
-        V3 acc = v3(0.0, 0.0, 0.0);
-        for (int s = 0; s < a.n_samples; ++s) {
-            const double* L = a.tail_buf + ((size_t)j * (size_t)a.n_samples + (size_t)s) * 3;
-            acc = acc + v3(L[0], L[1], L[2]) * a.inv_n;
-        }
         double* o = sub_buf + (size_t)(a.n_whole + j) * 3;
+        V3 acc = v3(o[0], o[1], o[2]);
+        const double* L = a.tail_buf + (size_t)j * (size_t)(a.n_samples - c0) * 3;
+        for (int s = c0; s < a.n_samples; ++s, L += 3) acc = acc + v3(L[0], L[1], L[2]) * a.inv_n;
         o[0] = acc.x;
         o[1] = acc.y;
         o[2] = acc.z;
@@ -316,6 +329,14 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, dou
     }
 #undef RT_MK_CASE
     return hipGetLastError();
+}
+
+// Scratch bytes one split subpixel needs (plan_tail: the samples after chunk 0, at the default chunk size).
+size_t tail_scratch_per_subpixel(int n_samples) {
+    RenderArgs a{};
+    a.n_samples = n_samples;
+    plan_tail(a, 0, 0, nullptr, 0);
+    return (size_t)std::max(0, n_samples - (1 << a.chunk_lg)) * 3 * sizeof(double);
 }
 
 void launch_tail_sum_f64(const RenderArgs& a, double* sub_buf, long n_split, hipStream_t st) {

@@ -461,8 +461,20 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
                         done = true;
                     }
                 }
-            } else {  // split tail (k_tail_sum_f64)
-                double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
+            } else if (tail_in_place(a, s)) {  // split tail, chunk 0: summed in place, its partial sum to sub_buf
+                V3 acc = v3(acc_l[0], acc_l[kBlk], acc_l[2 * kBlk]);
+                acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                acc_l[0] = acc.x; acc_l[kBlk] = acc.y; acc_l[2 * kBlk] = acc.z;
+                done = !unit_has_next(a, id, s);
+                if (done) {
+                    double* o = sub_buf + (size_t)id * 3;
+                    o[0] = acc.x;
+                    o[1] = acc.y;
+                    o[2] = acc.z;
+                }
+                ++s;
+            } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
+                double* o = tail_slot(a, id, s);
                 o[0] = ps.L.x;
                 o[1] = ps.L.y;
                 o[2] = ps.L.z;
@@ -734,8 +746,20 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
                         done = true;
                     }
                 }
-            } else {  // split tail (k_tail_sum_f64)
-                double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
+            } else if (tail_in_place(a, s)) {  // split tail, chunk 0: summed in place, its partial sum to sub_buf
+                V3 acc = v3(acc_l[0], acc_l[B], acc_l[2 * B]);
+                acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                acc_l[0] = acc.x; acc_l[B] = acc.y; acc_l[2 * B] = acc.z;
+                done = !unit_has_next(a, id, s);
+                if (done) {
+                    double* o = sub_buf + (size_t)id * 3;
+                    o[0] = acc.x;
+                    o[1] = acc.y;
+                    o[2] = acc.z;
+                }
+                ++s;
+            } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
+                double* o = tail_slot(a, id, s);
                 o[0] = ps.L.x;
                 o[1] = ps.L.y;
                 o[2] = ps.L.z;

@@ -614,8 +614,20 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
                             done = true;
                         }
                     }
-                } else {  // split tail (k_tail_sum_f64)
-                    double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
+                } else if (tail_in_place(a, s)) {  // split tail, chunk 0: summed in place, its partial sum to sub_buf
+                    V3 acc = v3(acc_l[0], acc_l[B], acc_l[2 * B]);
+                    acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                    acc_l[0] = acc.x; acc_l[B] = acc.y; acc_l[2 * B] = acc.z;
+                    done = !unit_has_next(a, id, s);
+                    if (done) {
+                        double* o = sub_buf + (size_t)id * 3;
+                        o[0] = acc.x;
+                        o[1] = acc.y;
+                        o[2] = acc.z;
+                    }
+                    ++s;
+                } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
+                    double* o = tail_slot(a, id, s);
                     o[0] = ps.L.x;
                     o[1] = ps.L.y;
                     o[2] = ps.L.z;
@@ -736,8 +748,20 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
                             done = true;
                         }
                     }
-                } else {  // split tail (k_tail_sum_f64)
-                    double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)a.n_samples + (size_t)s) * 3;
+                } else if (tail_in_place(a, s)) {  // split tail, chunk 0: summed in place, its partial sum to sub_buf
+                    V3 acc = v3(acc_l[0], acc_l[B], acc_l[2 * B]);
+                    acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                    acc_l[0] = acc.x; acc_l[B] = acc.y; acc_l[2 * B] = acc.z;
+                    done = !unit_has_next(a, id, s);
+                    if (done) {
+                        double* o = sub_buf + (size_t)id * 3;
+                        o[0] = acc.x;
+                        o[1] = acc.y;
+                        o[2] = acc.z;
+                    }
+                    ++s;
+                } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
+                    double* o = tail_slot(a, id, s);
                     o[0] = ps.L.x;
                     o[1] = ps.L.y;
                     o[2] = ps.L.z;
@@ -782,6 +806,399 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
     RT_DBG_TFLUSH();
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Role-split walk pool (P = 2, RT_MK_POOL=2): the block's waves are walkers or shaders, and paths are
+// not owned by threads. A block holds kRolePaths path slots in an LDS path store (SoA, RolePaths);
+// a path is either in a shader lane's registers, queued (ready queue: to be shaded; walk queue: its
+// closest or shadow query to be walked), or in a walker lane's registers while its query is walked.
+//   shader waves: every idle lane takes any ready path (queue_take_each) and loads it; a lane shades
+//     the hit its path holds, then traces the path's next ray (the same shade-then-trace order as the
+//     walk pool, P = 1); a query that needs an octree walk parks the path in the store, queues it for
+//     the walkers and frees the lane for the next ready path: vertex work runs on full waves instead of
+//     the ~32 of 64 lanes whose own path is not walking (profiles/r05a_dbg_mesh.log).
+//   walker waves: persistent walks (walk_step, one step per loop), each lane refilled from the walk
+//     queue as its walk ends; the walk state never leaves registers (no park: a query is parked only
+//     as its 68-B record before its first step), and a finished query's result goes into the store
+//     (closest: the hit; shadow: the NEE term added to L unless a mesh blocks it) before the path is
+//     queued as ready.
+// Every path computes the same values in the same order as k_megakernel_f64 / the walk pool (the
+// store keeps the doubles' bits), so frames are identical (tested).
+#ifndef RT_ROLES_WALKERS
+#define RT_ROLES_WALKERS 4  // walker waves of the 8 in a block
+#endif
+#ifndef RT_ROLES_REFILL
+#define RT_ROLES_REFILL 16  // a walker wave refills once at least this many of its lanes are idle
+#endif
+#ifndef RT_ROLES_PRIO
+#define RT_ROLES_PRIO 1  // walker waves at raised issue priority (their dependent loads issue first)
+#endif
+constexpr int kRoleWalkers = RT_ROLES_WALKERS;
+constexpr int kRoleWalkThreads = 64 * kRoleWalkers;
+constexpr int kRolePaths = kPoolThreads;  // path slots per block (a power of two: the queues' rings)
+static_assert(kRoleWalkers >= 1 && kRoleWalkers < kPoolThreads / 64, "walkers and shaders both needed");
+static_assert((kRolePaths & (kRolePaths - 1)) == 0, "the rings mask their index with kRolePaths - 1");
+// doubles: ray o, d; beta; L; subpixel accumulator; mirror state (bemit, o); query: shadow direction,
+// query t (closest: analytic hit t / result; shadow: distance), pending NEE term; pdf_prev (MIS)
+enum : int {
+    RD_O = 0, RD_D = 3, RD_B = 6, RD_L = 9, RD_A = 12, RD_E = 15, RD_C = 18, RD_QD = 21, RD_QT = 24, RD_PC = 25,
+    RD_PDF = 28, RD_N = 29
+};
+enum : int { RI_DEPTH = 0, RI_FLAGS = 1, RI_ID = 2, RI_S = 3, RI_HOBJ = 4, RI_HPRIM = 5, RI_NEAR = 6, RI_N = 7 };
+// RI_FLAGS: kind (2 bits), resume state << 2 (3 bits), closest query << 5, path continues << 6
+enum : int { RS_TRACE = 0, RS_SHADE = 1, RS_END = 2, RS_FRESH = 3 };
+struct RolePaths {
+    LdsDouble* d;  // [RD_N][kRolePaths]
+    LdsU64* u;     // [2][kRolePaths]: RNG state
+    LdsInt* i;     // [RI_N][kRolePaths]
+    RT_DEV LdsDouble& D(int f, int p) const { return d[f * kRolePaths + p]; }
+    RT_DEV LdsU64& U(int f, int p) const { return u[f * kRolePaths + p]; }
+    RT_DEV LdsInt& I(int f, int p) const { return i[f * kRolePaths + p]; }
+    RT_DEV V3 D3(int f, int p) const { return v3(D(f, p), D(f + 1, p), D(f + 2, p)); }
+    RT_DEV void set3(int f, int p, const V3& v) const { D(f, p) = v.x; D(f + 1, p) = v.y; D(f + 2, p) = v.z; }
+};
+// A shader lane's path in registers <-> the store. o: whether to store the ray origin (a shadow query's
+// sink already wrote its origin x there, the continuation's origin: the same bits when the path goes on).
+template <class C>
+RT_DEV void role_store(const RolePaths& P, int p, const PathState& ps, int id, int s, int flags, bool o) {
+    if (o) P.set3(RD_O, p, ps.ray.o);
+    P.set3(RD_D, p, ps.ray.d);
+    P.set3(RD_B, p, ps.beta);
+    P.set3(RD_L, p, ps.L);
+    if (!C::nospec && ps.kind == K_SPEC) {
+        P.set3(RD_E, p, ps.bemit);
+        P.set3(RD_C, p, ps.o);
+    }
+    if (C::mis) P.D(RD_PDF, p) = ps.pdf_prev;
+    P.U(0, p) = ps.r0;
+    P.U(1, p) = ps.r1;
+    P.I(RI_DEPTH, p) = (int32_t)ps.depth;
+    P.I(RI_FLAGS, p) = flags | ps.kind;
+    P.I(RI_ID, p) = id;
+    P.I(RI_S, p) = s;
+}
+template <class C>
+RT_DEV int role_load(const RolePaths& P, int p, PathState& ps, int& id, int& s) {
+    const int flags = P.I(RI_FLAGS, p);
+    ps.kind = flags & 3;
+    ps.ray = Ray{P.D3(RD_O, p), P.D3(RD_D, p)};
+    ps.beta = P.D3(RD_B, p);
+    ps.L = P.D3(RD_L, p);
+    if (!C::nospec && ps.kind == K_SPEC) {
+        ps.bemit = P.D3(RD_E, p);
+        ps.o = P.D3(RD_C, p);
+    }
+    ps.pdf_prev = C::mis ? P.D(RD_PDF, p) : 0.0;
+    ps.r0 = P.U(0, p);
+    ps.r1 = P.U(1, p);
+    ps.depth = (uint32_t)P.I(RI_DEPTH, p);
+    id = P.I(RI_ID, p);
+    s = P.I(RI_S, p);
+    return flags;
+}
+// The path slot p's closest query stays in the store while it waits for a walker (record: the analytic
+// hit so far and the near-mesh mask; the ray is the path's own).
+RT_DEV void role_query_closest(const RolePaths& P, int p, const HitRec& h, uint32_t near) {
+    P.D(RD_QT, p) = h.t;
+    P.I(RI_HOBJ, p) = h.obj;
+    P.I(RI_HPRIM, p) = h.prim;
+    P.I(RI_NEAR, p) = (int32_t)near;
+}
+
+template <int F, int W, bool S, int B = kPoolThreads>
+__global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, RenderArgs a_g, double* __restrict__ sub_buf,
+                                                                uint32_t* next_sub, long nsub) {
+    using C = Cfg<F | (RT_OPT_LDSOBJ ? kCfgLdsObj : 0)>;
+    static_assert(C::mesh && C::compact && !C::bvh, "the role-split pool walks octrees");
+    static_assert(B == kRolePaths && B % 64 == 0, "one path slot per thread of the block");
+#if RT_KARG_VIEW
+    const DevScene& sc = karg_scene();
+    const RenderArgs& a = karg_render_args();
+#else
+    const DevScene& sc = sc_g;
+    const RenderArgs& a = a_g;
+#endif
+    if constexpr (C::ldsobj) lds_objects_fill(sc);
+    __shared__ double s_pd[RD_N * kRolePaths];
+    __shared__ uint64_t s_pu[2 * kRolePaths];
+    __shared__ int32_t s_pi[RI_N * kRolePaths];
+    __shared__ int32_t s_ring[2][kRolePaths];  // [0] ready paths, [1] queued walks
+    __shared__ uint32_t s_qhead[2][2], s_qtail[2][2];
+    __shared__ int32_t s_anc[S ? kSlotAncLevels * kRoleWalkThreads : 1];  // walker lanes' ancestor columns
+    __shared__ uint32_t s_live;  // path slots still holding work (the block ends at 0)
+    const RolePaths P{(LdsDouble*)s_pd, (LdsU64*)s_pu, (LdsInt*)s_pi};
+    const LdsQueue rq{s_ring[0], s_qhead[0], s_qtail[0], (uint32_t)kRolePaths - 1u};
+    const LdsQueue wq{s_ring[1], s_qhead[1], s_qtail[1], (uint32_t)kRolePaths - 1u};
+    const long n_split = nsub - a.n_whole;
+    const long nunits = a.n_wunits + n_split * a.tail_cps;
+    // every path slot starts without a unit: queued as ready with RS_FRESH and id = -1 (a ticket first)
+    {
+        const int p = threadIdx.x;
+        P.I(RI_FLAGS, p) = RS_FRESH << 2;
+        P.I(RI_ID, p) = -1;
+        s_ring[0][p] = p;
+        s_ring[1][p] = -1;
+        if (p < 2) {
+            s_qhead[p][0] = 0; s_qhead[p][1] = 0;
+            s_qtail[p][0] = 0; s_qtail[p][1] = 0;
+        }
+        if (p == 0) {
+            s_qtail[0][0] = kRolePaths;
+            s_live = kRolePaths;
+        }
+    }
+    __syncthreads();
+    (void)s_qhead[0][1]; (void)s_qtail[0][1];
+    uint32_t nverts = 0;
+    RT_DBG_TINIT();
+    const bool walker = (int)(threadIdx.x >> 6) < kRoleWalkers;
+    if (walker) {
+        // ---- walker wave ----
+        LdsAncI32* anc = S ? (LdsAncI32*)s_anc + threadIdx.x : nullptr;
+        int32_t q = -1;
+        bool closest = false;
+        WalkRegs r;
+#if RT_ROLES_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
+        for (;;) {
+            RT_DBG_TSTART(t_it);
+            const int idle = __popcll(__ballot(q < 0));
+            if (idle >= RT_ROLES_REFILL || idle == 64) {
+                RT_DBG_TSTART(t_tk);
+                const int32_t q2 = queue_take_each(wq, q < 0);
+                if (q2 >= 0) {
+                    q = q2;
+                    const int flags = P.I(RI_FLAGS, q);
+                    closest = (flags >> 5) & 1;
+                    r.wr.o = P.D3(RD_O, q);
+                    r.wr.d = closest ? P.D3(RD_D, q) : P.D3(RD_QD, q);
+                    r.wi = make_inv(r.wr.d);
+                    r.wt = P.D(RD_QT, q);
+                    r.hobj = closest ? P.I(RI_HOBJ, q) : -1;
+                    r.hprim = closest ? P.I(RI_HPRIM, q) : -1;
+                    r.g = -1;
+                    r.w.cur = -1;
+                    r.occluded = 0;
+                }
+                RT_DBG_TEND(3, t_tk);
+                if (!__any(q >= 0)) {
+                    RT_DBG_TEND(0, t_it);
+                    if (__hip_atomic_load(&s_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    continue;
+                }
+            }
+            RT_DBG_TSTART(t_wk);
+            RT_DBG_WAVE(10, lane_id_is0());
+            RT_DBG_WAVE(11, q >= 0);
+            bool fin = false;
+            if (q >= 0) {
+                if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
+                    const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
+                    fin = !next_mesh_walk_near<C, S>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, (uint32_t)P.I(RI_NEAR, q));
+                }
+                if (!fin && r.w.cur >= 0) {
+                    double t;
+                    int prim;
+                    const int st = walk_step<S, kRoleWalkThreads, C::phong ? 0 : RT_WALK_HOIST>(sc, sc.meshes[r.mi], r.wr, r.wi,
+                                                                                             r.w, &t, &prim, anc);
+                    if (st != WALK_RUN) {
+                        if (closest) {
+                            if (st == WALK_HIT) {
+                                HitRec h{r.wt, r.hobj, r.hprim};
+                                consider(h, t, tables(sc)->gen_idx[r.g], prim);
+                                r.wt = h.t;
+                                r.hobj = h.obj;
+                                r.hprim = h.prim;
+                            }
+                        } else {
+                            r.occluded = st == WALK_HIT && !(t + 0.001 >= r.wt);  // mutually_visible's ERR_MARGIN
+                            fin = r.occluded;
+                        }
+                        r.w.cur = -1;
+                        fin |= r.g >= tables(sc)->last_mesh_g;  // no mesh left: the query's result is complete
+                    }
+                }
+                if (fin) {  // the result into the store, then the path to the ready queue
+                    const int flags = P.I(RI_FLAGS, q);
+                    int rs;
+                    if (closest) {
+                        P.D(RD_QT, q) = r.wt;
+                        P.I(RI_HOBJ, q) = r.hobj;
+                        P.I(RI_HPRIM, q) = r.hprim;
+                        rs = RS_SHADE;
+                    } else {
+                        if (!r.occluded) P.set3(RD_L, q, P.D3(RD_L, q) + P.D3(RD_PC, q));  // mutually_visible: the NEE term
+                        rs = ((flags >> 6) & 1) ? RS_TRACE : RS_END;
+                    }
+                    P.I(RI_FLAGS, q) = (flags & ~(7 << 2)) | (rs << 2);
+                }
+            }
+            RT_DBG_TEND(1, t_wk);
+            queue_put(rq, fin, q);
+            if (fin) q = -1;
+            RT_DBG_TEND(0, t_it);
+        }
+#if RT_ROLES_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
+    } else {
+        // ---- shader wave ----
+        int32_t p = -1;
+        PathState ps;
+        int id = 0, s = 0, rs = RS_FRESH;
+        bool cont = false;
+        HitRec hh{0.0, -1, -1};
+        for (;;) {
+            RT_DBG_TSTART(t_it);
+            RT_DBG_TSTART(t_tk);
+            if (__any(p < 0)) {
+                const int32_t q = queue_take_each(rq, p < 0);
+                if (q >= 0) {
+                    p = q;
+                    const int flags = role_load<C>(P, p, ps, id, s);
+                    rs = (flags >> 2) & 7;
+                    cont = (flags >> 6) & 1;
+                    if (rs == RS_SHADE) hh = HitRec{P.D(RD_QT, p), P.I(RI_HOBJ, p), P.I(RI_HPRIM, p)};
+                }
+            }
+            RT_DBG_TEND(3, t_tk);
+            if (!__any(p >= 0)) {
+                RT_DBG_TEND(0, t_it);
+                if (__hip_atomic_load(&s_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) break;
+                __builtin_amdgcn_s_sleep(2);
+                continue;
+            }
+            RT_DBG_TSTART(t_vx);
+            RT_DBG_WAVE(8, lane_id_is0());
+            RT_DBG_WAVE(9, p >= 0);
+            bool park = false, done = false;
+            if (p >= 0) {
+                bool sample_end = rs == RS_END;
+                if (rs == RS_SHADE) {
+                    nverts += hh.obj >= 0;
+                    ShadowDefer df;
+                    df.pending = false;
+                    RT_DBG_TSTART(t_sv);
+                    // a pending shadow query's origin, direction and distance go straight into the store
+                    const LdsQuerySink sink{&P.D(RD_O, p), &P.D(RD_QD, p), kRolePaths};
+                    cont = shade_vertex<C>(sc, a, ps, hh, &df, RegCold(), sink);
+                    RT_DBG_TEND(8, t_sv);
+                    if (df.pending) {  // a mesh could block the shadow ray: the walkers decide
+                        RT_DBG(12);
+                        P.set3(RD_PC, p, df.c);
+                        P.I(RI_NEAR, p) = (int32_t)df.meshes;
+                        role_store<C>(P, p, ps, id, s, (cont ? 1 << 6 : 0), false);
+                        park = true;
+                    } else if (!cont) {
+                        sample_end = true;
+                    } else {
+                        rs = RS_TRACE;
+                    }
+                }
+                if (sample_end) {
+                    if (id < a.n_whole) {
+                        V3 acc = P.D3(RD_A, p);
+                        acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                        P.set3(RD_A, p, acc);
+                        rs = RS_FRESH;
+                        if (++s == a.n_samples) {
+                            double* o = sub_buf + (size_t)id * 3;
+                            o[0] = acc.x;
+                            o[1] = acc.y;
+                            o[2] = acc.z;
+                            if (id + 1 < run_end(a, id)) {  // the next subpixel of the run, no ticket
+                                ++id;
+                                s = 0;
+                                P.set3(RD_A, p, v3(0.0, 0.0, 0.0));
+                            } else {
+                                done = true;
+                            }
+                        }
+                    } else if (tail_in_place(a, s)) {  // split tail, chunk 0: summed in place, its partial sum to sub_buf
+                        V3 acc = P.D3(RD_A, p);
+                        acc = acc + ps.L * a.inv_n;  // server.rs:357-358
+                        P.set3(RD_A, p, acc);
+                        rs = RS_FRESH;
+                        done = !unit_has_next(a, id, s);
+                        if (done) {
+                            double* o = sub_buf + (size_t)id * 3;
+                            o[0] = acc.x;
+                            o[1] = acc.y;
+                            o[2] = acc.z;
+                        }
+                        ++s;
+                    } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
+                        double* o = tail_slot(a, id, s);
+                        o[0] = ps.L.x;
+                        o[1] = ps.L.y;
+                        o[2] = ps.L.z;
+                        rs = RS_FRESH;
+                        done = !unit_has_next(a, id, s);
+                        ++s;
+                    }
+                }
+                if (rs == RS_FRESH && id < 0) done = true;  // a slot's first unit
+            }
+            // tickets: a path slot whose unit is done takes the next one; none left (or cancelled): it retires
+            bool stop = false;
+            if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+            const long nt = wave_ticket(next_sub, done && !stop);
+            if (__any(done)) flush_count(a.counters, nverts);
+            bool retire = false;
+            if (done) {
+                int end_unused;
+                unit_of(a, nt, id, end_unused, s);
+                P.set3(RD_A, p, v3(0.0, 0.0, 0.0));
+                retire = stop || nt >= nunits;
+            }
+            {
+                const unsigned long long m = __ballot(retire);
+                if (m && __lane_id() == __ffsll((long long)m) - 1)
+                    __hip_atomic_fetch_sub(&s_live, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (retire) p = -1;
+            // the next ray: the path going on, or its unit's next sample
+            if (p >= 0 && !park && (rs == RS_TRACE || rs == RS_FRESH)) {
+                if (rs == RS_FRESH) begin_sample(sc, a, subpixel_of(a, id), s, ps);
+                RT_DBG_TSTART(t_ta);
+                const RayInv wi = make_inv(ps.ray.d);
+                const HitRec h = trace_analytic<C>(sc, ps.ray, wi);
+                const uint32_t near = mesh_near_mask<C>(sc, ps.ray, wi, h.obj >= 0 ? h.t : INFINITY);
+                RT_DBG_TEND(6, t_ta);
+                if (near) {
+                    RT_DBG(13);
+                    role_query_closest(P, p, h, near);
+                    role_store<C>(P, p, ps, id, s, 1 << 5, true);
+                    park = true;
+                } else {
+                    hh = h;  // shaded in the next iteration
+                    rs = RS_SHADE;
+                }
+            }
+            queue_put(wq, park, p);
+            if (park) p = -1;
+            RT_DBG_TEND(2, t_vx);
+            RT_DBG_TEND(0, t_it);
+        }
+    }
+    flush_count(a.counters, nverts);
+    RT_DBG_TFLUSH();
+}
+
+template <int F, bool S = (RT_WALK_TIGHT != 0)>
+static void launch_roles(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub, long nsub,
+                         double* tail_buf, size_t tail_cap, hipStream_t st) {
+    constexpr int B = kPoolThreads;
+    const long blocks = resident_blocks(k_megakernel_roles_f64<F, 2, S>, (nsub + B - 1) / B, B);
+    RenderArgs a = a_in;
+    // the split tail and ticket runs planned for the lanes that hold paths (one path slot per thread)
+    plan_tail(a, nsub, blocks * B, tail_buf, tail_cap);
+    hipLaunchKernelGGL((k_megakernel_roles_f64<F, 2, S>), dim3((unsigned)blocks), dim3(B), 0, st, sc, a, sub_buf, next_sub,
+                       nsub);
+    launch_tail_sum_f64(a, sub_buf, nsub - a.n_whole, st);
+}
+
 template <int F, int W, int P, bool S = (RT_WALK_TIGHT != 0)>
 static void launch_mm(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub, long nsub,
                       int ksteps, int wmin, int refill, int pool_min, int pool_vmin, double* tail_buf, size_t tail_cap,
@@ -809,6 +1226,7 @@ hipError_t launch_megakernel_mesh_f64(const DevScene& sc, const RenderArgs& a, d
 #define RT_MM_CASE(F)                                                                          \
     case F:                                                                                    \
         if (!sc.node_slot) launch_mm<F, 2, 1, false>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, pool_refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
+        else if (pool == 2) launch_roles<F>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, st); \
         else if (pool) launch_mm<F, 2, 1>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, pool_refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
         else launch_mm<F, 2, 0>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, 0, 0, tail_buf, tail_cap, st); \
         break;

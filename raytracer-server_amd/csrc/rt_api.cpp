@@ -1047,9 +1047,10 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
         if (e == hipSuccess && a.n_samples <= 0) e = hipMemsetAsync(sub, 0, npix * 12 * sizeof(double), st);
         if (e == hipSuccess) {
             a.counters = ps ? ws->counters : nullptr;
-            // split-tail scratch: up to one subpixel per resident lane, at most 1.5 GB
-            const size_t per_sub = (size_t)std::max(0, a.n_samples) * 3 * sizeof(double);
-            const size_t want = std::min<size_t>((size_t)3 << 29, per_sub * std::min<size_t>(npix * 4 / 2, (size_t)1 << 19));
+            // split-tail scratch (megakernel_common.h plan_tail): the samples after chunk 0 of up to 2^18 split
+            // subpixels (plan_tail splits half a subpixel per resident lane: 2^17 on 256 CUs), at most 1.5 GB
+            const size_t per_sub = rt::tail_scratch_per_subpixel(a.n_samples);
+            const size_t want = std::min<size_t>((size_t)3 << 29, per_sub * std::min<size_t>(npix * 4 / 2, (size_t)1 << 18));
             if (!fp32 && per_sub > 0 && want >= per_sub) {
                 if (ws->ensure_tail(want) != hipSuccess) (void)hipGetLastError();  // no tail split then
             }
