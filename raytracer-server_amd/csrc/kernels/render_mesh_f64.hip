@@ -832,11 +832,19 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
 #ifndef RT_ROLES_PRIO
 #define RT_ROLES_PRIO 1  // walker waves at raised issue priority (their dependent loads issue first)
 #endif
+#ifndef RT_ROLES_BLOCK
+#define RT_ROLES_BLOCK 512  // threads of a block (one per CU: the path store takes the LDS); 768 = 3 waves/SIMD
+#endif
+#ifndef RT_ROLES_PATHS
+#define RT_ROLES_PATHS 512  // path slots per block (a power of two: the queues' rings)
+#endif
+constexpr int kRoleBlock = RT_ROLES_BLOCK;
 constexpr int kRoleWalkers = RT_ROLES_WALKERS;
 constexpr int kRoleWalkThreads = 64 * kRoleWalkers;
-constexpr int kRolePaths = kPoolThreads;  // path slots per block (a power of two: the queues' rings)
-static_assert(kRoleWalkers >= 1 && kRoleWalkers < kPoolThreads / 64, "walkers and shaders both needed");
-static_assert((kRolePaths & (kRolePaths - 1)) == 0, "the rings mask their index with kRolePaths - 1");
+constexpr int kRolePaths = RT_ROLES_PATHS;
+constexpr int kRoleRing = kRolePaths <= 256 ? 256 : kRolePaths <= 512 ? 512 : 1024;  // queue capacity (a power of two)
+static_assert(kRolePaths <= kRoleRing && kRoleRing <= 1024, "every path fits each queue once");
+static_assert(kRoleWalkers >= 1 && kRoleWalkers < kRoleBlock / 64, "walkers and shaders both needed");
 // doubles: ray o, d; beta; L; subpixel accumulator; mirror state (bemit, o); query: shadow direction,
 // query t (closest: analytic hit t / result; shadow: distance), pending NEE term; pdf_prev (MIS)
 enum : int {
@@ -904,12 +912,12 @@ RT_DEV void role_query_closest(const RolePaths& P, int p, const HitRec& h, uint3
     P.I(RI_NEAR, p) = (int32_t)near;
 }
 
-template <int F, int W, bool S, int B = kPoolThreads>
+template <int F, int W, bool S, int B = kRoleBlock>
 __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, RenderArgs a_g, double* __restrict__ sub_buf,
                                                                 uint32_t* next_sub, long nsub) {
     using C = Cfg<F | (RT_OPT_LDSOBJ ? kCfgLdsObj : 0)>;
     static_assert(C::mesh && C::compact && !C::bvh, "the role-split pool walks octrees");
-    static_assert(B == kRolePaths && B % 64 == 0, "one path slot per thread of the block");
+    static_assert(B % 64 == 0 && B <= 1024, "whole waves, at most 16 (path_f64.h: the diagnostic builds' per-wave LDS)");
 #if RT_KARG_VIEW
     const DevScene& sc = karg_scene();
     const RenderArgs& a = karg_render_args();
@@ -921,22 +929,26 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
     __shared__ double s_pd[RD_N * kRolePaths];
     __shared__ uint64_t s_pu[2 * kRolePaths];
     __shared__ int32_t s_pi[RI_N * kRolePaths];
-    __shared__ int32_t s_ring[2][kRolePaths];  // [0] ready paths, [1] queued walks
+    __shared__ int32_t s_ring[2][kRoleRing];  // [0] ready paths, [1] queued walks
     __shared__ uint32_t s_qhead[2][2], s_qtail[2][2];
     __shared__ int32_t s_anc[S ? kSlotAncLevels * kRoleWalkThreads : 1];  // walker lanes' ancestor columns
     __shared__ uint32_t s_live;  // path slots still holding work (the block ends at 0)
     const RolePaths P{(LdsDouble*)s_pd, (LdsU64*)s_pu, (LdsInt*)s_pi};
-    const LdsQueue rq{s_ring[0], s_qhead[0], s_qtail[0], (uint32_t)kRolePaths - 1u};
-    const LdsQueue wq{s_ring[1], s_qhead[1], s_qtail[1], (uint32_t)kRolePaths - 1u};
+    const LdsQueue rq{s_ring[0], s_qhead[0], s_qtail[0], (uint32_t)kRoleRing - 1u};
+    const LdsQueue wq{s_ring[1], s_qhead[1], s_qtail[1], (uint32_t)kRoleRing - 1u};
     const long n_split = nsub - a.n_whole;
     const long nunits = a.n_wunits + n_split * a.tail_cps;
     // every path slot starts without a unit: queued as ready with RS_FRESH and id = -1 (a ticket first)
+    for (int p = threadIdx.x; p < kRoleRing; p += B) {
+        if (p < kRolePaths) {
+            P.I(RI_FLAGS, p) = RS_FRESH << 2;
+            P.I(RI_ID, p) = -1;
+        }
+        s_ring[0][p] = p < kRolePaths ? p : -1;
+        s_ring[1][p] = -1;
+    }
     {
         const int p = threadIdx.x;
-        P.I(RI_FLAGS, p) = RS_FRESH << 2;
-        P.I(RI_ID, p) = -1;
-        s_ring[0][p] = p;
-        s_ring[1][p] = -1;
         if (p < 2) {
             s_qhead[p][0] = 0; s_qhead[p][1] = 0;
             s_qtail[p][0] = 0; s_qtail[p][1] = 0;
@@ -961,7 +973,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
         __builtin_amdgcn_s_setprio(1);
 #endif
         for (;;) {
-            RT_DBG_TSTART(t_it);
+            RT_DBG_TSTART(t_wi);
             const int idle = __popcll(__ballot(q < 0));
             if (idle >= RT_ROLES_REFILL || idle == 64) {
                 RT_DBG_TSTART(t_tk);
@@ -980,9 +992,9 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
                     r.w.cur = -1;
                     r.occluded = 0;
                 }
-                RT_DBG_TEND(3, t_tk);
+                RT_DBG_TEND(5, t_tk);
                 if (!__any(q >= 0)) {
-                    RT_DBG_TEND(0, t_it);
+                    RT_DBG_TEND(4, t_wi);
                     if (__hip_atomic_load(&s_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) break;
                     __builtin_amdgcn_s_sleep(2);
                     continue;
@@ -1037,7 +1049,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
             RT_DBG_TEND(1, t_wk);
             queue_put(rq, fin, q);
             if (fin) q = -1;
-            RT_DBG_TEND(0, t_it);
+            RT_DBG_TEND(4, t_wi);
         }
 #if RT_ROLES_PRIO
         __builtin_amdgcn_s_setprio(0);
@@ -1189,12 +1201,12 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
 template <int F, bool S = (RT_WALK_TIGHT != 0)>
 static void launch_roles(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub, long nsub,
                          double* tail_buf, size_t tail_cap, hipStream_t st) {
-    constexpr int B = kPoolThreads;
-    const long blocks = resident_blocks(k_megakernel_roles_f64<F, 2, S>, (nsub + B - 1) / B, B);
+    constexpr int B = kRoleBlock, W = kRoleBlock / 256;  // one block per CU: B / 256 waves per SIMD
+    const long blocks = resident_blocks(k_megakernel_roles_f64<F, W, S>, (nsub + B - 1) / B, B);
     RenderArgs a = a_in;
     // the split tail and ticket runs planned for the lanes that hold paths (one path slot per thread)
-    plan_tail(a, nsub, blocks * B, tail_buf, tail_cap);
-    hipLaunchKernelGGL((k_megakernel_roles_f64<F, 2, S>), dim3((unsigned)blocks), dim3(B), 0, st, sc, a, sub_buf, next_sub,
+    plan_tail(a, nsub, blocks * kRolePaths, tail_buf, tail_cap);
+    hipLaunchKernelGGL((k_megakernel_roles_f64<F, W, S>), dim3((unsigned)blocks), dim3(B), 0, st, sc, a, sub_buf, next_sub,
                        nsub);
     launch_tail_sum_f64(a, sub_buf, nsub - a.n_whole, st);
 }
@@ -1212,13 +1224,16 @@ static void launch_mm(const DevScene& sc, const RenderArgs& a_in, double* sub_bu
     launch_tail_sum_f64(a, sub_buf, nsub - a.n_whole, st);
 }
 
-// Octree walks through the block's walk pool, 2 waves/SIMD (3 waves/SIMD: 37 spilled VGPRs, measured 6%
-// slower; RT_MK_POOL=0: each lane walks its own query, RT_MK_KSTEPS steps per iteration).
+// Octree walks through the role-split pool (RT_MK_POOL=2, default) or the walk pool (1), 2 waves/SIMD (the walk
+// pool at 3 waves/SIMD: 37 spilled VGPRs, measured 6% slower; RT_MK_POOL=0: each lane walks its own query,
+// RT_MK_KSTEPS steps per iteration).
 // Scenes without slot tables (DevScene::node_slot null: node ids >= kSlotMaxNode) walk node_kids.
 hipError_t launch_megakernel_mesh_f64(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
                                       long nsub, int refill, int wmin, double* tail_buf, size_t tail_cap, hipStream_t st) {
     static const int ksteps = std::max(1, env_int("RT_MK_KSTEPS", 4));
-    static const int pool = env_int("RT_MK_POOL", 1);
+    // 2: the role-split pool (k_megakernel_roles_f64: unicorn 1920x1080x512 269.9 -> 310.6 Msamples/s,
+    // profiles/r05c_ab_c4.log); 1: the round-4 walk pool (every wave walks and shades its own paths); 0: per-lane walks
+    static const int pool = env_int("RT_MK_POOL", 2);
     static const int pool_min = env_int("RT_MK_POOL_MIN", 48);  // 48 with the 512-thread pool (32 before)
     static const int pool_ksteps = std::max(1, env_int("RT_MK_POOL_KSTEPS", 6));
     static const int pool_vmin = env_int("RT_MK_POOL_VMIN", 0);
