@@ -836,6 +836,33 @@ RT_DEV bool kid_tight_hit(const DevMesh& m, const int4& ks, const Ray& ray, cons
     axis((uint32_t)ks.z & 0xFFFFu, (uint32_t)ks.w >> 16, m.tight_base[2], ray.o.z, ray.d.z, inv.rz);
     return force || (keep && t0 <= t1);
 }
+// kid_tight_hit for rays whose direction components all lie in [2^-900, 2^900] in magnitude (every ray of
+// the wave: walk_node_slots' wave vote), where its `inr` holds on every axis, so `force` and `keep` keep
+// their initial values and every axis updates t0 / t1: the same operations on the same values, hence the
+// same result, without the per-axis range logic.
+#ifndef RT_TIGHT_FAST
+#define RT_TIGHT_FAST 1  // A/B: 0 = always the general form
+#endif
+RT_DEV bool kid_tight_hit_inr(const DevMesh& m, const int4& ks, const Ray& ray, const RayInv& inv) {
+    const double step = m.tight_step;
+    double t0 = 0.0, t1 = INFINITY;
+    auto axis = [&](uint32_t ql, uint32_t qh, double base, double o, double rc) {
+        const double lo = ql == 0u ? -INFINITY : fma((double)ql, step, base);
+        const double hi = qh == (uint32_t)kTightTop ? INFINITY : fma((double)qh, step, base);
+        const double ta = (lo - o) * rc, tb = (hi - o) * rc;
+        const double tn = fmin(ta, tb), tf = fmax(ta, tb);
+        t0 = fmax(t0, tn - 1e-9 * fabs(tn));
+        t1 = fmin(t1, tf + 1e-9 * fabs(tf));
+    };
+    axis((uint32_t)ks.y & 0xFFFFu, (uint32_t)ks.z >> 16, m.tight_base[0], ray.o.x, inv.rx);
+    axis((uint32_t)ks.y >> 16, (uint32_t)ks.w & 0xFFFFu, m.tight_base[1], ray.o.y, inv.ry);
+    axis((uint32_t)ks.z & 0xFFFFu, (uint32_t)ks.w >> 16, m.tight_base[2], ray.o.z, inv.rz);
+    return t0 <= t1;
+}
+RT_DEV bool dir_in_range(const Ray& ray) {  // kid_tight_hit's `inr` on all three axes
+    auto inr = [](double d) { return fabs(d) >= 0x1p-900 && fabs(d) <= 0x1p900; };
+    return inr(ray.d.x) && inr(ray.d.y) && inr(ray.d.z);
+}
 // The slot of child octant oi of node `cur` (one 16-byte load: entry + bounds).
 RT_DEV int4 kid_slot(const DevScene& sc, int32_t cur, uint32_t oi) {
     return *reinterpret_cast<const int4*>(sc.node_slot + 8 * (size_t)cur + oi);
@@ -969,6 +996,8 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
     // picks per step (a culled pick is as if the reference found nothing below that child)
     int32_t c = kKidEmpty;
     uint32_t oi = 0;
+    const bool inr = RT_TIGHT_FAST && wave_all(dir_in_range(ray));  // wave-uniform: one form of the test per step
+    auto tight = [&](const int4& ks) { return inr ? kid_tight_hit_inr(m, ks, ray, inv) : kid_tight_hit(m, ks, ray, inv); };
 #if RT_SLOT_PAIR
     if (!pf) {
         // both candidates' slots loaded at once (one row of node_slot: the same 128-byte line), so a
@@ -980,7 +1009,7 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
         const int4 ks2 = kid_slot(sc, w.cur, oi2);
         w.pm = pm1;
         oi = oi1;
-        if (!RT_SLOT_CULL || kid_tight_hit(m, ks1, ray, inv)) {
+        if (!RT_SLOT_CULL || tight(ks1)) {
             c = ks1.x;
         } else {
             RT_DBG(6);
@@ -990,7 +1019,7 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
             }
             w.pm &= w.pm - 1u;
             oi = oi2;
-            if (!kid_tight_hit(m, ks2, ray, inv)) {
+            if (!tight(ks2)) {
                 RT_DBG(6);
                 RT_DBG_TEND(14, t_pick);
                 return WALK_RUN;
@@ -1004,7 +1033,7 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
         w.pm &= w.pm - 1u;
         oi = (w.order >> (4 * q)) & 0xF;
         const int4 ks = (pf && pf->kind != 0 && tries == 0) ? pf->ks : kid_slot(sc, w.cur, oi);
-        if (!RT_SLOT_CULL || kid_tight_hit(m, ks, ray, inv)) {
+        if (!RT_SLOT_CULL || tight(ks)) {
             c = ks.x;
             break;
         }

@@ -808,7 +808,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
 
 // ---------------------------------------------------------------------------------------------------
 // Role-split walk pool (P = 2, RT_MK_POOL=2): the block's waves are walkers or shaders, and paths are
-// not owned by threads. A block holds kRolePaths path slots in an LDS path store (SoA, RolePaths);
+// not owned by threads. A block holds RoleLayout::paths path slots in an LDS path store (SoA, RolePaths);
 // a path is either in a shader lane's registers, queued (ready queue: to be shaded; walk queue: its
 // closest or shadow query to be walked), or in a walker lane's registers while its query is walked.
 //   shader waves: every idle lane takes any ready path (queue_take_each) and loads it; a lane shades
@@ -836,56 +836,73 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
 #define RT_ROLES_BLOCK 512  // threads of a block (one per CU: the path store takes the LDS); 768 = 3 waves/SIMD
 #endif
 #ifndef RT_ROLES_PATHS
-#define RT_ROLES_PATHS 512  // path slots per block (a power of two: the queues' rings)
+#define RT_ROLES_PATHS 512  // path slots per block (216 B each without MIS; 576 / 640 measured no faster, profiles/r05i_ab_np.log)
+#endif
+#ifndef RT_ROLES_PATHS_MIS
+#define RT_ROLES_PATHS_MIS 512  // ... with MIS (224 B each: pdf_prev)
 #endif
 constexpr int kRoleBlock = RT_ROLES_BLOCK;
 constexpr int kRoleWalkers = RT_ROLES_WALKERS;
 constexpr int kRoleWalkThreads = 64 * kRoleWalkers;
-constexpr int kRolePaths = RT_ROLES_PATHS;
-constexpr int kRoleRing = kRolePaths <= 256 ? 256 : kRolePaths <= 512 ? 512 : 1024;  // queue capacity (a power of two)
-static_assert(kRolePaths <= kRoleRing && kRoleRing <= 1024, "every path fits each queue once");
 static_assert(kRoleWalkers >= 1 && kRoleWalkers < kRoleBlock / 64, "walkers and shaders both needed");
-// doubles: ray o, d; beta; L; subpixel accumulator; mirror state (bemit, o); query: shadow direction,
-// query t (closest: analytic hit t / result; shadow: distance), pending NEE term; pdf_prev (MIS)
+// doubles: ray o, d; beta; L; subpixel accumulator; query: shadow direction, query t (closest: analytic hit
+// t / result; shadow: distance; LdsQuerySink's fourth column), pending NEE term; pdf_prev (MIS only).
+// The mirror state (bemit, o: RD_E, RD_C) shares the shadow query's columns: it is stored only when a
+// mirror vertex has been shaded (ps.kind == K_SPEC: no NEE there, so no shadow query) and read back into
+// registers when the path is loaded, before the next vertex's shading can write a shadow query.
 enum : int {
-    RD_O = 0, RD_D = 3, RD_B = 6, RD_L = 9, RD_A = 12, RD_E = 15, RD_C = 18, RD_QD = 21, RD_QT = 24, RD_PC = 25,
-    RD_PDF = 28, RD_N = 29
+    RD_O = 0, RD_D = 3, RD_B = 6, RD_L = 9, RD_A = 12, RD_QD = 15, RD_QT = 18, RD_PC = 19, RD_PDF = 22,
+    RD_E = RD_QD, RD_C = RD_PC
 };
-enum : int { RI_DEPTH = 0, RI_FLAGS = 1, RI_ID = 2, RI_S = 3, RI_HOBJ = 4, RI_HPRIM = 5, RI_NEAR = 6, RI_N = 7 };
-// RI_FLAGS: kind (2 bits), resume state << 2 (3 bits), closest query << 5, path continues << 6
+static_assert(RD_QT == RD_QD + 3, "LdsQuerySink writes the distance after the direction");
+template <class C>
+struct RoleLayout {
+    static constexpr int nd = C::mis ? RD_PDF + 1 : RD_PDF;  // doubles per path
+    static constexpr int paths = C::mis ? RT_ROLES_PATHS_MIS : RT_ROLES_PATHS;
+    static constexpr int ring = paths <= 256 ? 256 : paths <= 512 ? 512 : 1024;  // queue capacity (a power of two)
+    static_assert(paths <= ring && ring <= 1024, "every path fits each queue once");
+};
+// ints: flags | depth << 8, unit id, sample, closest query's hit object / prim, near-mesh mask
+enum : int { RI_FLAGS = 0, RI_ID = 1, RI_S = 2, RI_HOBJ = 3, RI_HPRIM = 4, RI_NEAR = 5, RI_N = 6 };
+// RI_FLAGS: kind (2 bits), resume state << 2 (3 bits), closest query << 5, path continues << 6, depth << 8
 enum : int { RS_TRACE = 0, RS_SHADE = 1, RS_END = 2, RS_FRESH = 3 };
+template <int NP>
 struct RolePaths {
-    LdsDouble* d;  // [RD_N][kRolePaths]
-    LdsU64* u;     // [2][kRolePaths]: RNG state
-    LdsInt* i;     // [RI_N][kRolePaths]
-    RT_DEV LdsDouble& D(int f, int p) const { return d[f * kRolePaths + p]; }
-    RT_DEV LdsU64& U(int f, int p) const { return u[f * kRolePaths + p]; }
-    RT_DEV LdsInt& I(int f, int p) const { return i[f * kRolePaths + p]; }
+    static constexpr int np = NP;
+    LdsDouble* d;  // [RoleLayout::nd][NP]
+    LdsU64* u;     // [2][NP]: RNG state
+    LdsInt* i;     // [RI_N][NP]
+    RT_DEV LdsDouble& D(int f, int p) const { return d[f * NP + p]; }
+    RT_DEV LdsU64& U(int f, int p) const { return u[f * NP + p]; }
+    RT_DEV LdsInt& I(int f, int p) const { return i[f * NP + p]; }
     RT_DEV V3 D3(int f, int p) const { return v3(D(f, p), D(f + 1, p), D(f + 2, p)); }
     RT_DEV void set3(int f, int p, const V3& v) const { D(f, p) = v.x; D(f + 1, p) = v.y; D(f + 2, p) = v.z; }
 };
-// A shader lane's path in registers <-> the store. o: whether to store the ray origin (a shadow query's
-// sink already wrote its origin x there, the continuation's origin: the same bits when the path goes on).
-template <class C>
-RT_DEV void role_store(const RolePaths& P, int p, const PathState& ps, int id, int s, int flags, bool o) {
-    if (o) P.set3(RD_O, p, ps.ray.o);
+// A shader lane's path in registers <-> the store. closest: the path parks for its closest query (the ray
+// origin is stored, and the mirror state if the path is at a mirror bounce); otherwise for a shadow query,
+// whose sink already wrote the origin x (the continuation's origin: the same bits when the path goes on)
+// and whose direction and NEE term hold the mirror state's columns. (A path parked for a shadow query
+// never needs the mirror state again: it continues from a diffuse vertex, or it has ended, in which case
+// ps.kind can still read K_SPEC, the kind it entered that vertex with.)
+template <class C, class RP>
+RT_DEV void role_store(const RP& P, int p, const PathState& ps, int id, int s, int flags, bool closest) {
+    if (closest) P.set3(RD_O, p, ps.ray.o);
     P.set3(RD_D, p, ps.ray.d);
     P.set3(RD_B, p, ps.beta);
     P.set3(RD_L, p, ps.L);
-    if (!C::nospec && ps.kind == K_SPEC) {
+    if (!C::nospec && closest && ps.kind == K_SPEC) {
         P.set3(RD_E, p, ps.bemit);
         P.set3(RD_C, p, ps.o);
     }
     if (C::mis) P.D(RD_PDF, p) = ps.pdf_prev;
     P.U(0, p) = ps.r0;
     P.U(1, p) = ps.r1;
-    P.I(RI_DEPTH, p) = (int32_t)ps.depth;
-    P.I(RI_FLAGS, p) = flags | ps.kind;
+    P.I(RI_FLAGS, p) = flags | ps.kind | (int32_t)(ps.depth << 8);
     P.I(RI_ID, p) = id;
     P.I(RI_S, p) = s;
 }
-template <class C>
-RT_DEV int role_load(const RolePaths& P, int p, PathState& ps, int& id, int& s) {
+template <class C, class RP>
+RT_DEV int role_load(const RP& P, int p, PathState& ps, int& id, int& s) {
     const int flags = P.I(RI_FLAGS, p);
     ps.kind = flags & 3;
     ps.ray = Ray{P.D3(RD_O, p), P.D3(RD_D, p)};
@@ -898,14 +915,15 @@ RT_DEV int role_load(const RolePaths& P, int p, PathState& ps, int& id, int& s) 
     ps.pdf_prev = C::mis ? P.D(RD_PDF, p) : 0.0;
     ps.r0 = P.U(0, p);
     ps.r1 = P.U(1, p);
-    ps.depth = (uint32_t)P.I(RI_DEPTH, p);
+    ps.depth = (uint32_t)flags >> 8;
     id = P.I(RI_ID, p);
     s = P.I(RI_S, p);
     return flags;
 }
 // The path slot p's closest query stays in the store while it waits for a walker (record: the analytic
 // hit so far and the near-mesh mask; the ray is the path's own).
-RT_DEV void role_query_closest(const RolePaths& P, int p, const HitRec& h, uint32_t near) {
+template <class RP>
+RT_DEV void role_query_closest(const RP& P, int p, const HitRec& h, uint32_t near) {
     P.D(RD_QT, p) = h.t;
     P.I(RI_HOBJ, p) = h.obj;
     P.I(RI_HPRIM, p) = h.prim;
@@ -926,25 +944,27 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
     const RenderArgs& a = a_g;
 #endif
     if constexpr (C::ldsobj) lds_objects_fill(sc);
-    __shared__ double s_pd[RD_N * kRolePaths];
-    __shared__ uint64_t s_pu[2 * kRolePaths];
-    __shared__ int32_t s_pi[RI_N * kRolePaths];
-    __shared__ int32_t s_ring[2][kRoleRing];  // [0] ready paths, [1] queued walks
+    using RL = RoleLayout<C>;
+    constexpr int NP = RL::paths, kRing = RL::ring;
+    __shared__ double s_pd[RL::nd * NP];
+    __shared__ uint64_t s_pu[2 * NP];
+    __shared__ int32_t s_pi[RI_N * NP];
+    __shared__ int32_t s_ring[2][kRing];  // [0] ready paths, [1] queued walks
     __shared__ uint32_t s_qhead[2][2], s_qtail[2][2];
     __shared__ int32_t s_anc[S ? kSlotAncLevels * kRoleWalkThreads : 1];  // walker lanes' ancestor columns
     __shared__ uint32_t s_live;  // path slots still holding work (the block ends at 0)
-    const RolePaths P{(LdsDouble*)s_pd, (LdsU64*)s_pu, (LdsInt*)s_pi};
-    const LdsQueue rq{s_ring[0], s_qhead[0], s_qtail[0], (uint32_t)kRoleRing - 1u};
-    const LdsQueue wq{s_ring[1], s_qhead[1], s_qtail[1], (uint32_t)kRoleRing - 1u};
+    const RolePaths<NP> P{(LdsDouble*)s_pd, (LdsU64*)s_pu, (LdsInt*)s_pi};
+    const LdsQueue rq{s_ring[0], s_qhead[0], s_qtail[0], (uint32_t)kRing - 1u};
+    const LdsQueue wq{s_ring[1], s_qhead[1], s_qtail[1], (uint32_t)kRing - 1u};
     const long n_split = nsub - a.n_whole;
     const long nunits = a.n_wunits + n_split * a.tail_cps;
     // every path slot starts without a unit: queued as ready with RS_FRESH and id = -1 (a ticket first)
-    for (int p = threadIdx.x; p < kRoleRing; p += B) {
-        if (p < kRolePaths) {
+    for (int p = threadIdx.x; p < kRing; p += B) {
+        if (p < NP) {
             P.I(RI_FLAGS, p) = RS_FRESH << 2;
             P.I(RI_ID, p) = -1;
         }
-        s_ring[0][p] = p < kRolePaths ? p : -1;
+        s_ring[0][p] = p < NP ? p : -1;
         s_ring[1][p] = -1;
     }
     {
@@ -954,8 +974,8 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
             s_qtail[p][0] = 0; s_qtail[p][1] = 0;
         }
         if (p == 0) {
-            s_qtail[0][0] = kRolePaths;
-            s_live = kRolePaths;
+            s_qtail[0][0] = NP;
+            s_live = NP;
         }
     }
     __syncthreads();
@@ -1093,7 +1113,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
                     df.pending = false;
                     RT_DBG_TSTART(t_sv);
                     // a pending shadow query's origin, direction and distance go straight into the store
-                    const LdsQuerySink sink{&P.D(RD_O, p), &P.D(RD_QD, p), kRolePaths};
+                    const LdsQuerySink sink{&P.D(RD_O, p), &P.D(RD_QD, p), NP};
                     cont = shade_vertex<C>(sc, a, ps, hh, &df, RegCold(), sink);
                     RT_DBG_TEND(8, t_sv);
                     if (df.pending) {  // a mesh could block the shadow ray: the walkers decide
@@ -1205,7 +1225,7 @@ static void launch_roles(const DevScene& sc, const RenderArgs& a_in, double* sub
     const long blocks = resident_blocks(k_megakernel_roles_f64<F, W, S>, (nsub + B - 1) / B, B);
     RenderArgs a = a_in;
     // the split tail and ticket runs planned for the lanes that hold paths (one path slot per thread)
-    plan_tail(a, nsub, blocks * kRolePaths, tail_buf, tail_cap);
+    plan_tail(a, nsub, blocks * RoleLayout<Cfg<F>>::paths, tail_buf, tail_cap);
     hipLaunchKernelGGL((k_megakernel_roles_f64<F, W, S>), dim3((unsigned)blocks), dim3(B), 0, st, sc, a, sub_buf, next_sub,
                        nsub);
     launch_tail_sum_f64(a, sub_buf, nsub - a.n_whole, st);

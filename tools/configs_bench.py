@@ -141,7 +141,13 @@ for label, name, w, h, spp, mis in CONFIGS:
                          "algorithmic_model": "SURVEY 8(d): 88 B per camera sample + 280 B per path vertex"}}
     if name != "cornell_box" and not fp32:
         wc = walk_counters(name, w, h, mis, spp)
-        if wc and wc["vertices"] and wc["calls"]:  # (flat meshes, the cubes: flat_query, no walk counters)
+        if wc and wc["vertices"] and wc["calls"] and not (wc["parent_visits"] or wc["leaves"] or wc["tri_tests"]):
+            # flat meshes (the cubes): flat_query reads its mesh's triangles through scalar loads, outside the walk
+            # counters, so the octree model has nothing to count
+            line["roofline"]["scene_bytes"] = None
+            line["roofline"]["scene_bytes_note"] = ("not applicable: every mesh is a flat octree, queried by flat_query "
+                                                    "(scalar loads of <= 32 triangles per mesh), not walked")
+        elif wc and wc["vertices"] and wc["calls"]:
             per_v = {k: wc[k] / wc["vertices"] for k in ("calls", "parent_visits", "leaves", "tri_tests")}
             sb_v = 32 * per_v["parent_visits"] + 8 * per_v["leaves"] + 40 * per_v["tri_tests"]
             line["roofline"]["scene_bytes"] = {
@@ -156,6 +162,7 @@ for label, name, w, h, spp, mis in CONFIGS:
         rf = line["roofline"]
         rf["compute"] = bench.compute_block(pmc["valu_mix"], st["vertices"], st["device_ms"])
         rf["compute"]["source"] = src
+        rf["compute"]["kernel"] = pmc.get("kernel")
         if pmc.get("waits"):
             rf["compute"]["simd_valu_busy"] = round(pmc["waits"]["simd_valu_busy"], 4)
             rf["compute"]["wait_any"] = round(pmc["waits"]["wait_any"], 4)
