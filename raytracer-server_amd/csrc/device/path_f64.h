@@ -631,6 +631,7 @@ struct OctWalk {
 
 // LDS column of a walk's ancestor node ids (walk_node_slots' `anc`)
 typedef __attribute__((address_space(3))) int32_t LdsAncI32;
+typedef __attribute__((address_space(3))) uint16_t LdsAncU16;  // pids < 2^16 (DevScene::n_pid): half the LDS
 
 // Mask `cur`'s existing children whose boxes the ray hits, permuted to visiting order (the node_kids
 // walk: the child table is read again by each pick, an L2 hit).
@@ -898,8 +899,8 @@ struct SlotPF {
     uint32_t pm;
     int kind;
 };
-template <int AS = 256>
-RT_DEV void slot_prefetch(const DevScene& sc, const OctWalk& w, const LdsAncI32* anc, SlotPF& pf) {
+template <int AS = 256, class Anc = LdsAncI32>
+RT_DEV void slot_prefetch(const DevScene& sc, const OctWalk& w, const Anc* anc, SlotPF& pf) {
     pf.kind = 0;
     if (w.enter) return;
     uint32_t pm = w.pm;
@@ -912,7 +913,7 @@ RT_DEV void slot_prefetch(const DevScene& sc, const OctWalk& w, const LdsAncI32*
         }
         if (pm == 0) return;
         if (anc) {
-            cur = anc[lv * AS];
+            cur = (int32_t)anc[lv * AS];
         } else {
             for (int l = w.depth; l > lv; --l) cur = sc.pid_up[cur];
         }
@@ -929,9 +930,9 @@ RT_DEV void slot_prefetch(const DevScene& sc, const OctWalk& w, const LdsAncI32*
     pf.pm = pm;
     pf.ks = *reinterpret_cast<const int4*>(sc.node_slot + 8 * (size_t)cur + ((w.order >> (4 * __builtin_ctz(pm))) & 0xF));
 }
-template <int AS = 256>  // `anc`'s stride (the block's threads)
+template <int AS = 256, class Anc = LdsAncI32>  // `anc`'s stride (the block's threads) and element type
 RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w,
-                           LdsAncI32* anc = nullptr, const SlotPF* pf = nullptr) {
+                           Anc* anc = nullptr, const SlotPF* pf = nullptr) {
     RT_DBG_TSTART(t_pop);
     uint32_t exist = 0;  // a node to enter: its existence mask (the root at a walk's start, or a descent)
     if (w.enter) {
@@ -957,7 +958,7 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
             return WALK_MISS;
         }
         if (anc) {
-            w.cur = anc[lv * AS];
+            w.cur = (int32_t)anc[lv * AS];
         } else {  // the parent chain by pid (rows of node_slot / node_box)
             int32_t cur = w.cur;
             for (int l = w.depth; l > lv; --l) cur = sc.pid_up[cur];
@@ -1065,7 +1066,7 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
     }
     // descend: push the remaining mask of `cur`, take the octant's box
     const int lv = w.depth;
-    if (anc) anc[lv * AS] = w.cur;
+    if (anc) anc[lv * AS] = w.cur;  // (a pid: < 2^16 for a 16-bit column)
     if (lv < 8) w.stk = (w.stk & ~(0xFFull << (8 * lv))) | ((uint64_t)w.pm << (8 * lv));
     else w.stk8 = w.pm;
     w.path |= oi << (3 * lv);
@@ -1164,9 +1165,9 @@ RT_DEV int walk_node(const DevScene& sc, const DevMesh& m, const Ray& ray, const
 // walk inlined there trips an AMDGPU backend error, "illegal VGPR to SGPR copy", in ROCm 7.2.)
 // Hoist: RT_WALK_HOIST's modes (below); the Phong / mesh-light instances of the walk pool pass 0, where
 // the hoisted triangles' registers would spill.
-template <bool Slots = (RT_WALK_TIGHT != 0), int AS = 256, int Hoist = RT_WALK_HOIST>
+template <bool Slots = (RT_WALK_TIGHT != 0), int AS = 256, int Hoist = RT_WALK_HOIST, class Anc = LdsAncI32>
 RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const RayInv& inv, OctWalk& w, double* t,
-                     int* prim, LdsAncI32* anc = nullptr) {
+                     int* prim, Anc* anc = nullptr) {
     RT_DBG(5);
     if constexpr (Slots) {
         // The node walk and the triangle tests run in the same step, one leaf apart: the node walk
@@ -1194,9 +1195,9 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         SlotPF pf;
         pf.kind = 0;
         if constexpr (Hoist == 2) {
-            if (!w.ndone) slot_prefetch<AS>(sc, w, anc, pf);
+            if (!w.ndone) slot_prefetch<AS, Anc>(sc, w, anc, pf);
         } else {
-            if (!w.ndone && w.nlf >= w.nle && walk_node_slots<AS>(sc, m, ray, inv, w, anc) == WALK_MISS) w.ndone = 1;
+            if (!w.ndone && w.nlf >= w.nle && walk_node_slots<AS, Anc>(sc, m, ray, inv, w, anc) == WALK_MISS) w.ndone = 1;
         }
         RT_DBG_TSTART(t_lt);
         if (Hoist != 0 ? open : w.lpos < w.lend) {
@@ -1215,7 +1216,7 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         }
         RT_DBG_TEND(12, t_lt);
         if constexpr (Hoist == 2) {
-            if (!w.ndone && w.nlf >= w.nle && walk_node_slots<AS>(sc, m, ray, inv, w, anc, &pf) == WALK_MISS) w.ndone = 1;
+            if (!w.ndone && w.nlf >= w.nle && walk_node_slots<AS, Anc>(sc, m, ray, inv, w, anc, &pf) == WALK_MISS) w.ndone = 1;
         }
         return w.ndone && w.lpos >= w.lend && w.nlf >= w.nle ? WALK_MISS : WALK_RUN;
     }

@@ -222,7 +222,8 @@ struct DevScene {
                                 // arithmetic: a pop of the slot walk reloads the ancestor's box from here
     const int32_t* pid_up;      // [pid] the parent's parent as a pid (-1 at a root): the pops of slot walks
                                 // without an LDS ancestor column (node_up is indexed by node id)
-    int32_t pad6, pad7;
+    int32_t n_pid;              // rows of node_slot / node_box / pid_up (parents of all octrees)
+    int32_t pad7;
     float off32;                // f32 mode: hit points are offset by off32 * n (scene-scaled epsilon)
     int32_t n_objects, light, n_meshes, compact;
     double cam_pos[3], cam_dir[3];

@@ -824,7 +824,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
 // Every path computes the same values in the same order as k_megakernel_f64 / the walk pool (the
 // store keeps the doubles' bits), so frames are identical (tested).
 #ifndef RT_ROLES_WALKERS
-#define RT_ROLES_WALKERS 4  // walker waves of the 8 in a block
+#define RT_ROLES_WALKERS 6  // walker waves of the block's 12
 #endif
 #ifndef RT_ROLES_REFILL
 #define RT_ROLES_REFILL 16  // a walker wave refills once at least this many of its lanes are idle
@@ -833,25 +833,39 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
 #define RT_ROLES_PRIO 1  // walker waves at raised issue priority (their dependent loads issue first)
 #endif
 #ifndef RT_ROLES_BLOCK
-#define RT_ROLES_BLOCK 512  // threads of a block (one per CU: the path store takes the LDS); 768 = 3 waves/SIMD
+#define RT_ROLES_BLOCK 768  // threads of a block (one per CU: the path store takes the LDS): 3 waves/SIMD (168 VGPRs);
+                            // 512 threads (2 waves/SIMD) with 512 paths measured 17% slower (profiles/r05l_ab_b768.log)
 #endif
+// Path slots per block: as many as the LDS holds besides the queues, the walkers' ancestor columns and the
+// object table (192 B each without MIS, 200 with). Throughput rises with the paths in flight (each waits
+// ~14 walk steps per walk): 576 -> 632 slots +8.3% at 768 threads (profiles/r05l_ab_b768.log)
 #ifndef RT_ROLES_PATHS
-#define RT_ROLES_PATHS 512  // path slots per block (216 B each without MIS; 576 / 640 measured no faster, profiles/r05i_ab_np.log)
+#define RT_ROLES_PATHS 752
 #endif
 #ifndef RT_ROLES_PATHS_MIS
-#define RT_ROLES_PATHS_MIS 512  // ... with MIS (224 B each: pdf_prev)
+#define RT_ROLES_PATHS_MIS 720
 #endif
-constexpr int kRoleBlock = RT_ROLES_BLOCK;
-constexpr int kRoleWalkers = RT_ROLES_WALKERS;
-constexpr int kRoleWalkThreads = 64 * kRoleWalkers;
-static_assert(kRoleWalkers >= 1 && kRoleWalkers < kRoleBlock / 64, "walkers and shaders both needed");
-// doubles: ray o, d; beta; L; subpixel accumulator; query: shadow direction, query t (closest: analytic hit
-// t / result; shadow: distance; LdsQuerySink's fourth column), pending NEE term; pdf_prev (MIS only).
+#ifndef RT_ANC16
+#define RT_ANC16 1  // the walkers' ancestor columns hold 16-bit pids (scenes with more parents pop through pid_up)
+#endif
+using AncT = std::conditional_t<RT_ANC16 != 0, uint16_t, int32_t>;
+// Block shape per instance: the Phong instances (the Phong BRDF's shading code: 32 spilled VGPRs at the
+// 168 of 3 waves/SIMD) keep 512-thread blocks, 2 waves/SIMD, half of them walkers.
+template <class C>
+struct RoleShape {
+    static constexpr int block = C::phong ? 512 : RT_ROLES_BLOCK;
+    static constexpr int walkers = C::phong ? 4 : RT_ROLES_WALKERS;
+    static constexpr int walk_threads = 64 * walkers;
+    static_assert(walkers >= 1 && walkers < block / 64, "walkers and shaders both needed");
+};
+// doubles: ray o, d; beta; L; query: shadow direction, query t (closest: analytic hit t / result; shadow:
+// distance; LdsQuerySink's fourth column), pending NEE term; pdf_prev (MIS only). (A slot's running sum
+// over its unit's samples is kept in the unit's sub_buf entry, not here: role_sample_end.)
 // The mirror state (bemit, o: RD_E, RD_C) shares the shadow query's columns: it is stored only when a
 // mirror vertex has been shaded (ps.kind == K_SPEC: no NEE there, so no shadow query) and read back into
 // registers when the path is loaded, before the next vertex's shading can write a shadow query.
 enum : int {
-    RD_O = 0, RD_D = 3, RD_B = 6, RD_L = 9, RD_A = 12, RD_QD = 15, RD_QT = 18, RD_PC = 19, RD_PDF = 22,
+    RD_O = 0, RD_D = 3, RD_B = 6, RD_L = 9, RD_QD = 12, RD_QT = 15, RD_PC = 16, RD_PDF = 19,
     RD_E = RD_QD, RD_C = RD_PC
 };
 static_assert(RD_QT == RD_QD + 3, "LdsQuerySink writes the distance after the direction");
@@ -930,7 +944,7 @@ RT_DEV void role_query_closest(const RP& P, int p, const HitRec& h, uint32_t nea
     P.I(RI_NEAR, p) = (int32_t)near;
 }
 
-template <int F, int W, bool S, int B = kRoleBlock>
+template <int F, int W, bool S, int B = RoleShape<Cfg<F>>::block>
 __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, RenderArgs a_g, double* __restrict__ sub_buf,
                                                                 uint32_t* next_sub, long nsub) {
     using C = Cfg<F | (RT_OPT_LDSOBJ ? kCfgLdsObj : 0)>;
@@ -951,7 +965,10 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
     __shared__ int32_t s_pi[RI_N * NP];
     __shared__ int32_t s_ring[2][kRing];  // [0] ready paths, [1] queued walks
     __shared__ uint32_t s_qhead[2][2], s_qtail[2][2];
-    __shared__ int32_t s_anc[S ? kSlotAncLevels * kRoleWalkThreads : 1];  // walker lanes' ancestor columns
+    using RS = RoleShape<C>;
+    static_assert(RS::block == B, "the launch's block shape");
+    // walker lanes' ancestor columns: 16-bit pids (RT_ANC16) when the scene's pids fit, else the pid_up chain
+    __shared__ AncT s_anc[S ? kSlotAncLevels * RS::walk_threads : 1];
     __shared__ uint32_t s_live;  // path slots still holding work (the block ends at 0)
     const RolePaths<NP> P{(LdsDouble*)s_pd, (LdsU64*)s_pu, (LdsInt*)s_pi};
     const LdsQueue rq{s_ring[0], s_qhead[0], s_qtail[0], (uint32_t)kRing - 1u};
@@ -982,10 +999,11 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
     (void)s_qhead[0][1]; (void)s_qtail[0][1];
     uint32_t nverts = 0;
     RT_DBG_TINIT();
-    const bool walker = (int)(threadIdx.x >> 6) < kRoleWalkers;
+    const bool walker = (int)(threadIdx.x >> 6) < RS::walkers;
     if (walker) {
         // ---- walker wave ----
-        LdsAncI32* anc = S ? (LdsAncI32*)s_anc + threadIdx.x : nullptr;
+        using LdsAnc = __attribute__((address_space(3))) AncT;
+        LdsAnc* anc = S && (!RT_ANC16 || sc.n_pid <= 0x10000) ? (LdsAnc*)s_anc + threadIdx.x : nullptr;
         int32_t q = -1;
         bool closest = false;
         WalkRegs r;
@@ -1032,7 +1050,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
                 if (!fin && r.w.cur >= 0) {
                     double t;
                     int prim;
-                    const int st = walk_step<S, kRoleWalkThreads, C::phong ? 0 : RT_WALK_HOIST>(sc, sc.meshes[r.mi], r.wr, r.wi,
+                    const int st = walk_step<S, RS::walk_threads, C::phong ? 0 : RT_WALK_HOIST>(sc, sc.meshes[r.mi], r.wr, r.wi,
                                                                                              r.w, &t, &prim, anc);
                     if (st != WALK_RUN) {
                         if (closest) {
@@ -1129,43 +1147,36 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
                     }
                 }
                 if (sample_end) {
-                    if (id < a.n_whole) {
-                        V3 acc = P.D3(RD_A, p);
-                        acc = acc + ps.L * a.inv_n;  // server.rs:357-358
-                        P.set3(RD_A, p, acc);
-                        rs = RS_FRESH;
-                        if (++s == a.n_samples) {
-                            double* o = sub_buf + (size_t)id * 3;
-                            o[0] = acc.x;
-                            o[1] = acc.y;
-                            o[2] = acc.z;
-                            if (id + 1 < run_end(a, id)) {  // the next subpixel of the run, no ticket
-                                ++id;
-                                s = 0;
-                                P.set3(RD_A, p, v3(0.0, 0.0, 0.0));
-                            } else {
-                                done = true;
+                    rs = RS_FRESH;
+                    if (id < a.n_whole || tail_in_place(a, s)) {
+                        // a whole subpixel, or the split tail's chunk 0: the running sum acc + L * inv_n from 0
+                        // (server.rs:357-358) in the subpixel's sub_buf entry (the partial sum of chunk 0 is what
+                        // k_tail_sum_f64 continues from)
+                        double* o = sub_buf + (size_t)id * 3;
+                        V3 acc = v3(0.0, 0.0, 0.0);
+                        if (s != 0) acc = v3(o[0], o[1], o[2]);
+                        acc = acc + ps.L * a.inv_n;
+                        o[0] = acc.x;
+                        o[1] = acc.y;
+                        o[2] = acc.z;
+                        if (id < a.n_whole) {
+                            if (++s == a.n_samples) {
+                                if (id + 1 < run_end(a, id)) {  // the next subpixel of the run, no ticket
+                                    ++id;
+                                    s = 0;
+                                } else {
+                                    done = true;
+                                }
                             }
+                        } else {
+                            done = !unit_has_next(a, id, s);
+                            ++s;
                         }
-                    } else if (tail_in_place(a, s)) {  // split tail, chunk 0: summed in place, its partial sum to sub_buf
-                        V3 acc = P.D3(RD_A, p);
-                        acc = acc + ps.L * a.inv_n;  // server.rs:357-358
-                        P.set3(RD_A, p, acc);
-                        rs = RS_FRESH;
-                        done = !unit_has_next(a, id, s);
-                        if (done) {
-                            double* o = sub_buf + (size_t)id * 3;
-                            o[0] = acc.x;
-                            o[1] = acc.y;
-                            o[2] = acc.z;
-                        }
-                        ++s;
                     } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
                         double* o = tail_slot(a, id, s);
                         o[0] = ps.L.x;
                         o[1] = ps.L.y;
                         o[2] = ps.L.z;
-                        rs = RS_FRESH;
                         done = !unit_has_next(a, id, s);
                         ++s;
                     }
@@ -1181,7 +1192,6 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
             if (done) {
                 int end_unused;
                 unit_of(a, nt, id, end_unused, s);
-                P.set3(RD_A, p, v3(0.0, 0.0, 0.0));
                 retire = stop || nt >= nunits;
             }
             {
@@ -1221,7 +1231,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
 template <int F, bool S = (RT_WALK_TIGHT != 0)>
 static void launch_roles(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub, long nsub,
                          double* tail_buf, size_t tail_cap, hipStream_t st) {
-    constexpr int B = kRoleBlock, W = kRoleBlock / 256;  // one block per CU: B / 256 waves per SIMD
+    constexpr int B = RoleShape<Cfg<F>>::block, W = B / 256;  // one block per CU: B / 256 waves per SIMD
     const long blocks = resident_blocks(k_megakernel_roles_f64<F, W, S>, (nsub + B - 1) / B, B);
     RenderArgs a = a_in;
     // the split tail and ticket runs planned for the lanes that hold paths (one path slot per thread)

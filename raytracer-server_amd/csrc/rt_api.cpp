@@ -752,6 +752,7 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.node_slot = p.slots.empty() ? nullptr : (const rt::KidSlot*)(b + o_slot);
         ds.node_box = p.slots.empty() ? nullptr : (const double*)(b + o_nbox);
         ds.pid_up = p.slots.empty() ? nullptr : (const int32_t*)(b + o_pup);
+        ds.n_pid = p.slots.empty() ? 0 : (int32_t)p.pid_up.size();
         ds.light = s->host.light;
         ds.light_pdf = 0.0;
         if (ds.light >= 0 && ds.light < (int32_t)p.objects.size()) {
