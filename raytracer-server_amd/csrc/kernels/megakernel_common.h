@@ -117,20 +117,27 @@ __device__ unsigned long long g_qcheck[4];
 // head / tail counters. The caller guarantees that no more than mask + 1 entries are ever queued
 // at once (each query of a block is in the queue at most once). Entries are written after the tail
 // is advanced, so a taker waits for its entry to turn non-negative; it then resets it to -1.
-struct LdsQueue {
-    int32_t* ring;
+template <class E>
+struct LdsQueueT {
+    using T = E;
+    E* ring;         // entries (>= 0), -1 = empty slot; int32_t, or int16_t for queues of < 2^15 entries
     uint32_t* head;  // next entry to take
     uint32_t* tail;  // next entry to fill
     uint32_t mask;   // capacity - 1 (a power of two)
 };
+using LdsQueue = LdsQueueT<int32_t>;
+using LdsQueue16 = LdsQueueT<int16_t>;  // the role-split pool's path ids: half the ring's LDS
 // Entries queued and not yet claimed (head read first: the tail read after it is >= it, so the
 // difference never wraps).
-__device__ __forceinline__ uint32_t queue_len(const LdsQueue& q) {
+template <class Q>
+__device__ __forceinline__ uint32_t queue_len(const Q& q) {
     const uint32_t h = __hip_atomic_load(q.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return __hip_atomic_load(q.tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) - h;
 }
 // Appends v of every lane with `put` (wave-aggregated). All lanes of the wave call.
-__device__ __forceinline__ void queue_put(const LdsQueue& q, bool put, int32_t v) {
+template <class Q>
+__device__ __forceinline__ void queue_put(const Q& q, bool put, int32_t v) {
+    using T = typename Q::T;
     const unsigned long long m = __ballot(put);
     if (m == 0ull) return;
     const int lane = __lane_id();
@@ -146,17 +153,18 @@ __device__ __forceinline__ void queue_put(const LdsQueue& q, bool put, int32_t v
         if ((int32_t)(base + (uint32_t)__popcll(m) - h) > (int32_t)(q.mask + 1u)) RT_QFAIL(1);
     }
     if (put) {
-        const int32_t old = __hip_atomic_exchange(&q.ring[(base + (uint32_t)__popcll(below)) & q.mask], v, __ATOMIC_RELEASE,
-                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+        const T old = __hip_atomic_exchange(&q.ring[(base + (uint32_t)__popcll(below)) & q.mask], (T)v, __ATOMIC_RELEASE,
+                                            __HIP_MEMORY_SCOPE_WORKGROUP);
         if (old != -1) RT_QFAIL(0);
     }
 #else
-    if (put) __hip_atomic_store(&q.ring[(base + (uint32_t)__popcll(below)) & q.mask], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (put) __hip_atomic_store(&q.ring[(base + (uint32_t)__popcll(below)) & q.mask], (T)v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 #endif
 }
 // Claims up to `most` entries, but only if at least max(need, 1) are queued; the leader lane does the
 // compare-and-swap. Returns the first claimed position and the count (wave-uniform).
-__device__ __forceinline__ void queue_claim(const LdsQueue& q, int leader, uint32_t most, int need, uint32_t& h, uint32_t& k) {
+template <class Q>
+__device__ __forceinline__ void queue_claim(const Q& q, int leader, uint32_t most, int need, uint32_t& h, uint32_t& k) {
     h = 0;
     k = 0;
     if (__lane_id() == leader) {
@@ -175,23 +183,27 @@ __device__ __forceinline__ void queue_claim(const LdsQueue& q, int leader, uint3
     h = __shfl(h, leader, 64);
     k = __shfl(k, leader, 64);
 }
-__device__ __forceinline__ int32_t queue_read(const LdsQueue& q, uint32_t pos) {
-    int32_t* e = &q.ring[pos & q.mask];
-    int32_t v;
+template <class Q>
+__device__ __forceinline__ int32_t queue_read(const Q& q, uint32_t pos) {
+    using T = typename Q::T;
+    T* e = &q.ring[pos & q.mask];
+    T v;
     while ((v = __hip_atomic_load(e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < 0) __builtin_amdgcn_s_sleep(1);
-    __hip_atomic_store(e, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(e, (T)-1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (RT_QCHECK && (uint32_t)v > q.mask) RT_QFAIL(0);  // entries (lane ids, + 256 for fpool shadow queries) < capacity
-    return v;
+    return (int32_t)v;
 }
 // Takes up to 64 entries (lane i the i-th), but only if at least `need` are queued; -1 for lanes
 // without one. All lanes of the wave call.
-__device__ __forceinline__ int32_t queue_take(const LdsQueue& q, int need) {
+template <class Q>
+__device__ __forceinline__ int32_t queue_take(const Q& q, int need) {
     uint32_t h, k;
     queue_claim(q, 0, 64u, need, h, k);
     return (uint32_t)__lane_id() < k ? queue_read(q, h + (uint32_t)__lane_id()) : -1;
 }
 // Every lane with `want` takes one entry while any are queued (-1 otherwise). All lanes call.
-__device__ __forceinline__ int32_t queue_take_each(const LdsQueue& q, bool want) {
+template <class Q>
+__device__ __forceinline__ int32_t queue_take_each(const Q& q, bool want) {
     const unsigned long long m = __ballot(want);
     if (m == 0ull) return -1;
     const int lane = __lane_id();

@@ -839,11 +839,16 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
 // Path slots per block: as many as the LDS holds besides the queues, the walkers' ancestor columns and the
 // object table (192 B each without MIS, 200 with). Throughput rises with the paths in flight (each waits
 // ~14 walk steps per walk): 576 -> 632 slots +8.3% at 768 threads (profiles/r05l_ab_b768.log)
+#if RT_DEBUG_COUNTERS || RT_DEBUG_TIMERS
+#define RT_ROLES_DBG_LDS 16  // the diagnostic builds' per-block counters and timers take ~2.4 KB of LDS
+#else
+#define RT_ROLES_DBG_LDS 0
+#endif
 #ifndef RT_ROLES_PATHS
-#define RT_ROLES_PATHS 752
+#define RT_ROLES_PATHS (784 - RT_ROLES_DBG_LDS)
 #endif
 #ifndef RT_ROLES_PATHS_MIS
-#define RT_ROLES_PATHS_MIS 720
+#define RT_ROLES_PATHS_MIS (752 - RT_ROLES_DBG_LDS)
 #endif
 #ifndef RT_ANC16
 #define RT_ANC16 1  // the walkers' ancestor columns hold 16-bit pids (scenes with more parents pop through pid_up)
@@ -876,9 +881,14 @@ struct RoleLayout {
     static constexpr int ring = paths <= 256 ? 256 : paths <= 512 ? 512 : 1024;  // queue capacity (a power of two)
     static_assert(paths <= ring && ring <= 1024, "every path fits each queue once");
 };
-// ints: flags | depth << 8, unit id, sample, closest query's hit object / prim, near-mesh mask
-enum : int { RI_FLAGS = 0, RI_ID = 1, RI_S = 2, RI_HOBJ = 3, RI_HPRIM = 4, RI_NEAR = 5, RI_N = 6 };
-// RI_FLAGS: kind (2 bits), resume state << 2 (3 bits), closest query << 5, path continues << 6, depth << 8
+// ints: flags, unit id, sample, closest query's hit prim, near-mesh mask
+enum : int { RI_FLAGS = 0, RI_ID = 1, RI_S = 2, RI_HPRIM = 3, RI_NEAR = 4, RI_N = 5 };
+// RI_FLAGS: kind (2 bits), resume state << 2 (3 bits), closest query << 5, path continues << 6, the closest
+// query's hit object + 1 << 7 (5 bits: compact scenes hold <= 16 objects), depth << 12
+constexpr int kRfObj = 7, kRfDepth = 12;
+static_assert(kMaxCompactObjects < 31, "a hit object id + 1 fits 5 bits");
+RT_DEV int32_t rf_obj(int32_t obj) { return (obj + 1) << kRfObj; }
+RT_DEV int32_t rf_get_obj(int flags) { return ((flags >> kRfObj) & 31) - 1; }
 enum : int { RS_TRACE = 0, RS_SHADE = 1, RS_END = 2, RS_FRESH = 3 };
 template <int NP>
 struct RolePaths {
@@ -911,7 +921,7 @@ RT_DEV void role_store(const RP& P, int p, const PathState& ps, int id, int s, i
     if (C::mis) P.D(RD_PDF, p) = ps.pdf_prev;
     P.U(0, p) = ps.r0;
     P.U(1, p) = ps.r1;
-    P.I(RI_FLAGS, p) = flags | ps.kind | (int32_t)(ps.depth << 8);
+    P.I(RI_FLAGS, p) = flags | ps.kind | (int32_t)(ps.depth << kRfDepth);
     P.I(RI_ID, p) = id;
     P.I(RI_S, p) = s;
 }
@@ -929,17 +939,17 @@ RT_DEV int role_load(const RP& P, int p, PathState& ps, int& id, int& s) {
     ps.pdf_prev = C::mis ? P.D(RD_PDF, p) : 0.0;
     ps.r0 = P.U(0, p);
     ps.r1 = P.U(1, p);
-    ps.depth = (uint32_t)flags >> 8;
+    ps.depth = (uint32_t)flags >> kRfDepth;
     id = P.I(RI_ID, p);
     s = P.I(RI_S, p);
     return flags;
 }
 // The path slot p's closest query stays in the store while it waits for a walker (record: the analytic
-// hit so far and the near-mesh mask; the ray is the path's own).
+// hit so far and the near-mesh mask; the ray is the path's own; the hit object goes into the flags that
+// role_store writes, rf_obj).
 template <class RP>
 RT_DEV void role_query_closest(const RP& P, int p, const HitRec& h, uint32_t near) {
     P.D(RD_QT, p) = h.t;
-    P.I(RI_HOBJ, p) = h.obj;
     P.I(RI_HPRIM, p) = h.prim;
     P.I(RI_NEAR, p) = (int32_t)near;
 }
@@ -963,7 +973,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
     __shared__ double s_pd[RL::nd * NP];
     __shared__ uint64_t s_pu[2 * NP];
     __shared__ int32_t s_pi[RI_N * NP];
-    __shared__ int32_t s_ring[2][kRing];  // [0] ready paths, [1] queued walks
+    __shared__ int16_t s_ring[2][kRing];  // [0] ready paths, [1] queued walks (path ids < 1024)
     __shared__ uint32_t s_qhead[2][2], s_qtail[2][2];
     using RS = RoleShape<C>;
     static_assert(RS::block == B, "the launch's block shape");
@@ -971,8 +981,8 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
     __shared__ AncT s_anc[S ? kSlotAncLevels * RS::walk_threads : 1];
     __shared__ uint32_t s_live;  // path slots still holding work (the block ends at 0)
     const RolePaths<NP> P{(LdsDouble*)s_pd, (LdsU64*)s_pu, (LdsInt*)s_pi};
-    const LdsQueue rq{s_ring[0], s_qhead[0], s_qtail[0], (uint32_t)kRing - 1u};
-    const LdsQueue wq{s_ring[1], s_qhead[1], s_qtail[1], (uint32_t)kRing - 1u};
+    const LdsQueue16 rq{s_ring[0], s_qhead[0], s_qtail[0], (uint32_t)kRing - 1u};
+    const LdsQueue16 wq{s_ring[1], s_qhead[1], s_qtail[1], (uint32_t)kRing - 1u};
     const long n_split = nsub - a.n_whole;
     const long nunits = a.n_wunits + n_split * a.tail_cps;
     // every path slot starts without a unit: queued as ready with RS_FRESH and id = -1 (a ticket first)
@@ -1024,7 +1034,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
                     r.wr.d = closest ? P.D3(RD_D, q) : P.D3(RD_QD, q);
                     r.wi = make_inv(r.wr.d);
                     r.wt = P.D(RD_QT, q);
-                    r.hobj = closest ? P.I(RI_HOBJ, q) : -1;
+                    r.hobj = closest ? rf_get_obj(flags) : -1;
                     r.hprim = closest ? P.I(RI_HPRIM, q) : -1;
                     r.g = -1;
                     r.w.cur = -1;
@@ -1072,16 +1082,17 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
                 if (fin) {  // the result into the store, then the path to the ready queue
                     const int flags = P.I(RI_FLAGS, q);
                     int rs;
+                    int fl = flags & ~(7 << 2);
                     if (closest) {
                         P.D(RD_QT, q) = r.wt;
-                        P.I(RI_HOBJ, q) = r.hobj;
                         P.I(RI_HPRIM, q) = r.hprim;
+                        fl = (fl & ~(31 << kRfObj)) | rf_obj(r.hobj);
                         rs = RS_SHADE;
                     } else {
                         if (!r.occluded) P.set3(RD_L, q, P.D3(RD_L, q) + P.D3(RD_PC, q));  // mutually_visible: the NEE term
                         rs = ((flags >> 6) & 1) ? RS_TRACE : RS_END;
                     }
-                    P.I(RI_FLAGS, q) = (flags & ~(7 << 2)) | (rs << 2);
+                    P.I(RI_FLAGS, q) = fl | (rs << 2);
                 }
             }
             RT_DBG_TEND(1, t_wk);
@@ -1109,7 +1120,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
                     const int flags = role_load<C>(P, p, ps, id, s);
                     rs = (flags >> 2) & 7;
                     cont = (flags >> 6) & 1;
-                    if (rs == RS_SHADE) hh = HitRec{P.D(RD_QT, p), P.I(RI_HOBJ, p), P.I(RI_HPRIM, p)};
+                    if (rs == RS_SHADE) hh = HitRec{P.D(RD_QT, p), rf_get_obj(flags), P.I(RI_HPRIM, p)};
                 }
             }
             RT_DBG_TEND(3, t_tk);
@@ -1211,7 +1222,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
                 if (near) {
                     RT_DBG(13);
                     role_query_closest(P, p, h, near);
-                    role_store<C>(P, p, ps, id, s, 1 << 5, true);
+                    role_store<C>(P, p, ps, id, s, 1 << 5 | rf_obj(h.obj), true);
                     park = true;
                 } else {
                     hh = h;  // shaded in the next iteration
