@@ -1055,7 +1055,9 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
             if (q >= 0) {
                 if (r.w.cur < 0) {  // begin the walk of the next candidate mesh (none left: done)
                     const double tmax = closest ? (r.hobj >= 0 ? r.wt : INFINITY) : r.wt;
+                    RT_DBG_TSTART(t_bg);
                     fin = !next_mesh_walk_near<C, S>(sc, r.wr, r.wi, tmax, r.g, r.mi, r.w, (uint32_t)P.I(RI_NEAR, q));
+                    RT_DBG_TEND(15, t_bg);
                 }
                 if (!fin && r.w.cur >= 0) {
                     double t;

@@ -70,9 +70,11 @@ def walk_counters(scene, w, h, mis, spp):
 
 
 def _round_key(f):
-    """Sort key of profiles/r<NN><tag>_pmc_*.json files: newest round (then tag) last."""
+    """Sort key of profiles/r<NN><tag>_pmc_*.json files: newest round, then newest tag, last (tags run a..z,
+    then aa..az: a longer tag is newer)."""
     b = os.path.basename(f)
-    return (b[1:3], b.split("_pmc_")[0], b)
+    tag = b.split("_pmc_")[0][3:]
+    return (b[1:3], len(tag), tag, b)
 
 
 def pmc_summary(scene, w, h, spp, mis):
