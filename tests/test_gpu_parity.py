@@ -383,6 +383,34 @@ def test_two_deep_meshes_parity(rt, oracle, tmp_path):
         _assert_parity(rgb_g, sub_g, rgb_o, sub_o, f"two meshes/{'mk' if mk else 'wf'}")
 
 
+@pytest.mark.parametrize("phong", [False, True], ids=["diffuse", "phong"])
+def test_deep_mesh_mis_and_phong_parity(phong, rt, oracle, tmp_path):
+    """The role-split pool's other instances on a deep octree (chair.obj): MIS on and off (the 768-thread
+    instances with and without pdf_prev in the path record), and with Phong objects (a Phong floor and a
+    Phong sphere: the 512-thread instances, render_mesh_f64.hip RoleShape), against the oracle at the
+    1e-9 / RGB8 bounds (scene.rs:56-98 Phong lobes, scene.rs:186-215 MIS)."""
+    from test_host_prep import extra_asset_scene
+
+    p = extra_asset_scene(tmp_path, "chair.obj")
+    text = open(p).read()
+    if phong:
+        floor = 'brdf = { type = "diffuse", kd = [0.75, 0.75, 0.75] }\ngeometry = { type = "plane", pos = [0.0, 0.0, 0.0], n = [0.0, 1.0, 0.0] }'
+        assert floor in text
+        text = text.replace(floor, floor.replace('{ type = "diffuse", kd = [0.75, 0.75, 0.75] }', '{ type = "phong", kd = 0.5, '
+                                                 'ks = 0.3, power = 8, color_d = [0.7, 0.6, 0.5], color_s = [1.0, 1.0, 1.0] }'))
+        text += ('[[objects]]\nbrdf = { type = "phong", kd = 0.2, ks = 0.7, power = 24, color_d = [0.9, 0.3, 0.3], '
+                 'color_s = [1.0, 1.0, 1.0] }\ngeometry = { type = "sphere", pos = [22.0, 12.0, 60.0], r = 12.0 }\n')
+        open(p, "w").write(text)
+    sc, orc = rt.Scene.from_toml(p), oracle.OracleScene(p)
+    assert len(sc.mesh(5)["kind"]) >= 64  # a deep octree: the role-split pool walks it
+    w, h, spp = 64, 48, 8
+    for mis in (False, True):
+        rgb_o, sub_o, st_o = orc.render(w, h, spp, SEED, mis=mis)
+        rgb_g, sub_g, st = rt.render(sc, w, h, spp, SEED, megakernel=True, mis=mis, want_sub=True)
+        assert 0.9 * st_o["vertices"] <= st["vertices"] <= st_o["vertices"]
+        _assert_parity(rgb_g, sub_g, rgb_o, sub_o, f"chair/{'phong' if phong else 'diffuse'}/{'mis' if mis else 'nee'}")
+
+
 # ---------------------------------------------------------------- reference quirks off the 3 scenes
 QUIRK_SCENE = """
 [camera]

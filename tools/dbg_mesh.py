@@ -37,7 +37,7 @@ if scene != "cubes":  # the walk-pool kernel (render_mesh_f64.hip, path_f64.h wa
     T.update({3: "pool: take + park load", 5: "pool: park store + put", 6: "vertex: trace + mesh cull",
               8: "vertex: shade_vertex", 12: "walk: leaf triangles", 13: "walk: pop", 14: "walk: pick + descend",
               15: "walk: begin (root order)"})
-if os.environ.get("RT_MK_POOL") == "2" and scene != "cubes":  # the role-split pool (k_megakernel_roles_f64)
+if os.environ.get("RT_MK_POOL", "2") == "2" and scene != "cubes":  # the role-split pool (default) (k_megakernel_roles_f64)
     T.update({0: "shader: iteration", 1: "walker: walk step", 2: "shader: vertex work", 3: "shader: take + load",
               4: "walker: iteration", 5: "walker: refill"})
     print(f"  roles: shader iterations {c[8]}, lanes holding a path {c[9] / it:.1f}; walker steps {c[10]}, "
