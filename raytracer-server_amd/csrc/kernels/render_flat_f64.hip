@@ -514,8 +514,10 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
 // in fuller chunks, and no wave waits at a barrier for another wave's chunk (the block-synchronous
 // kernel spent 24% of its wave time in barrier waits, 2 waves of 4 working in phase P).
 #ifndef RT_FPOOL_BLOCK
-#define RT_FPOOL_BLOCK 768  // threads per query-pool block of the no-mirror instance: one block per CU (12 waves
-                            // share one query queue per mesh), or 256 (three blocks per CU, A/B)
+#define RT_FPOOL_BLOCK 1024  // threads per query-pool block of the no-mirror instance: one block per CU (16 waves,
+                             // 4 per SIMD, share one query queue per mesh; 128 VGPRs, 36 spilled): cubes +9.8% over
+                             // 768 (3 waves/SIMD, profiles/r05w_ab_fp.log), which the running sums in sub_buf and
+                             // the 16-bit rings made fit the LDS; or 256 (three blocks per CU, A/B)
 #endif
 #ifndef RT_FPOOL_PRIO
 #define RT_FPOOL_PRIO 1  // the query chunks (stage 1) at raised issue priority (s_setprio 1: cubes +1.3%, r04ao), or not (0)
@@ -544,7 +546,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
     const RenderArgs& a = a_g;
 #endif
     lds_objects_fill(sc);
-    // per lane (one column per thread): subpixel accumulator; the closest-hit query ray (o, d), the
+    // per lane (one column per thread): the closest-hit query ray (o, d), the
     // shadow query ray (o, d, |y - x|); results per (mesh, lane); queries outstanding per lane
     // The closest-hit and the shadow query of a lane are issued in the same iteration from the same
     // point (the shadow ray's x and the next ray's origin, integrator_f64.h shade_vertex; a camera ray
@@ -553,7 +555,6 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
     // t, and the hit triangle as its index within the mesh (flat meshes hold <= kFlatMaxTris). The
     // mirror-bounce state (o, pre-bounce throughput) lives in LDS as in k_megakernel_f64 (LdsCold):
     // 12 VGPRs less at 3 waves/SIMD.
-    __shared__ double s_acc[3 * B];
     __shared__ double s_qo[3 * B], s_qdc[3 * B], s_qds[4 * B];
     __shared__ double s_rt[kFlatMeshes * B];
     __shared__ uint8_t s_rp[kFlatMeshes * B];
@@ -572,7 +573,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
     bool nvalid = false;  // nbd / nbr hold sample s + 1 of subpixel id
     __shared__ int32_t s_pend[B];
     // per mesh: queued queries, entry = lane (closest hit) or 256 + lane (shadow)
-    __shared__ int32_t s_ring[kFlatMeshes][kRing];
+    __shared__ int16_t s_ring[kFlatMeshes][kRing];  // entries < 2 B <= 2048
     __shared__ uint32_t s_head[kFlatMeshes], s_tail[kFlatMeshes];
     const int tid = threadIdx.x;
     for (int i = tid; i < kFlatMeshes * kRing; i += B) (&s_ring[0][0])[i] = -1;
@@ -583,7 +584,6 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
     s_pend[tid] = 0;
     RT_DBG_TINIT();
     __syncthreads();
-    LdsD* acc_l = (LdsD*)s_acc + tid;
     const int nm = sc.n_meshes;
 
     uint32_t nverts = 0;
@@ -593,7 +593,6 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
     const long t0 = wave_ticket(next_sub, true);
     unit_of(a, t0, id, end, s);
     bool active = t0 < nunits;
-    acc_l[0] = 0.0; acc_l[B] = 0.0; acc_l[2 * B] = 0.0;
     PathState ps;
     bool fresh = true;
     bool traced = false;   // ps.ray has been traced: h is its analytic hit, qmask its closest-hit queries
@@ -615,7 +614,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
             // paths wait (also the frame's end: no query waits for a quorum that never comes)
             const int need = __popcll(__ballot(rdy)) >= RT_FPOOL_READY ? pool_min : 1;
             for (int m = 0; m < nm; ++m) {
-                const LdsQueue Q{s_ring[m], &s_head[m], &s_tail[m], (uint32_t)kRing - 1u};
+                const LdsQueue16 Q{s_ring[m], &s_head[m], &s_tail[m], (uint32_t)kRing - 1u};
                 const int32_t e = queue_take(Q, need);
                 if (!__any(e >= 0)) continue;
                 RT_DBG_WAVE(13, lane_id_is0());
@@ -729,35 +728,30 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
         bool done = false;
         if (finish) {
             fresh = true;
-            if (id < a.n_whole) {
-                V3 acc = v3(acc_l[0], acc_l[B], acc_l[2 * B]);
-                acc = acc + ps.L * a.inv_n;  // server.rs:357-358
-                acc_l[0] = acc.x; acc_l[B] = acc.y; acc_l[2 * B] = acc.z;
-                if (++s == a.n_samples) {
-                    double* o = sub_buf + (size_t)id * 3;
-                    o[0] = acc.x;
-                    o[1] = acc.y;
-                    o[2] = acc.z;
-                    if (++id < end) {  // the next subpixel of the run, no ticket
-                        s = 0;
-                        acc_l[0] = 0.0; acc_l[B] = 0.0; acc_l[2 * B] = 0.0;
-                        nvalid = false;
-                    } else {
-                        done = true;
+            if (id < a.n_whole || tail_in_place(a, s)) {
+                // a whole subpixel, or the split tail's chunk 0: the running sum acc + L * inv_n from 0
+                // (server.rs:357-358) kept in the subpixel's sub_buf entry (read back: the same bits), which
+                // frees the LDS column it took
+                double* o = sub_buf + (size_t)id * 3;
+                V3 acc = v3(0.0, 0.0, 0.0);
+                if (s != 0) acc = v3(o[0], o[1], o[2]);
+                acc = acc + ps.L * a.inv_n;
+                o[0] = acc.x;
+                o[1] = acc.y;
+                o[2] = acc.z;
+                if (id < a.n_whole) {
+                    if (++s == a.n_samples) {
+                        if (++id < end) {  // the next subpixel of the run, no ticket
+                            s = 0;
+                            nvalid = false;
+                        } else {
+                            done = true;
+                        }
                     }
+                } else {
+                    done = !unit_has_next(a, id, s);
+                    ++s;
                 }
-            } else if (tail_in_place(a, s)) {  // split tail, chunk 0: summed in place, its partial sum to sub_buf
-                V3 acc = v3(acc_l[0], acc_l[B], acc_l[2 * B]);
-                acc = acc + ps.L * a.inv_n;  // server.rs:357-358
-                acc_l[0] = acc.x; acc_l[B] = acc.y; acc_l[2 * B] = acc.z;
-                done = !unit_has_next(a, id, s);
-                if (done) {
-                    double* o = sub_buf + (size_t)id * 3;
-                    o[0] = acc.x;
-                    o[1] = acc.y;
-                    o[2] = acc.z;
-                }
-                ++s;
             } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
                 double* o = tail_slot(a, id, s);
                 o[0] = ps.L.x;
@@ -774,7 +768,6 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
         if (done) {
             unit_of(a, nt, id, end, s);
             active = !stop && nt < nunits;
-            acc_l[0] = 0.0; acc_l[B] = 0.0; acc_l[2 * B] = 0.0;
             fresh = true;
             nvalid = false;
         }
@@ -824,7 +817,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
             RT_QFAIL(3);
         if (want_s | want_c) s_pend[tid] = __popc(want_s) + __popc(want_c);
         for (int m = 0; m < nm; ++m) {
-            const LdsQueue Q{s_ring[m], &s_head[m], &s_tail[m], (uint32_t)kRing - 1u};
+            const LdsQueue16 Q{s_ring[m], &s_head[m], &s_tail[m], (uint32_t)kRing - 1u};
             queue_put(Q, (want_s >> m) & 1u, B + tid);
             queue_put(Q, (want_c >> m) & 1u, tid);
         }
@@ -877,8 +870,8 @@ hipError_t launch_megakernel_flat_f64(const DevScene& sc, const RenderArgs& a_in
         break;
     if (fpool && nospec && (a.features & 32) && !(a.features & 2)) {  // no mirror, no Phong object
         switch (a.features & 15) {
-            case 9: launch_fpool<9 | 32, 3, RT_FPOOL_BLOCK>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); break;
-            case 13: launch_fpool<13 | 32, 3, RT_FPOOL_BLOCK>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); break;
+            case 9: launch_fpool<9 | 32, RT_FPOOL_BLOCK / 256, RT_FPOOL_BLOCK>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); break;
+            case 13: launch_fpool<13 | 32, RT_FPOOL_BLOCK / 256, RT_FPOOL_BLOCK>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); break;
             default: return hipErrorInvalidValue;
         }
     } else {

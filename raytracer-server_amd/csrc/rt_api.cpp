@@ -753,6 +753,9 @@ int upload(rt_scene* s, int device, rt::DevScene* out) {
         ds.node_box = p.slots.empty() ? nullptr : (const double*)(b + o_nbox);
         ds.pid_up = p.slots.empty() ? nullptr : (const int32_t*)(b + o_pup);
         ds.n_pid = p.slots.empty() ? 0 : (int32_t)p.pid_up.size();
+        // RT_TEST_ANC_OFF (tests only): report more pids than a 16-bit ancestor column holds, so the role
+        // pool's walkers pop through pid_up (the path of octrees with > 65536 parents)
+        if (std::getenv("RT_TEST_ANC_OFF") && ds.n_pid > 0) ds.n_pid = 0x7FFFFFFF;
         ds.light = s->host.light;
         ds.light_pdf = 0.0;
         if (ds.light >= 0 && ds.light < (int32_t)p.objects.size()) {

@@ -153,7 +153,7 @@ def _cull_run(lib=None, env=None):
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
-@pytest.mark.parametrize("variant", ["walkref", "near64", "noslots"])
+@pytest.mark.parametrize("variant", ["walkref", "near64", "noslots", "noanc"])
 def test_walk_culls_do_not_change_frames(variant):
     """The culls the mesh kernels add to the reference's octree walk (geometry.rs:1262-1273) are exact:
     the cubes (C3) and the unicorn (C4) at 1920x1080 render byte-identical frames without them —
@@ -161,7 +161,9 @@ def test_walk_culls_do_not_change_frames(variant):
                (-DRT_WALK_TIGHT=0, lib/variants/walkref.so: node_kids walks);
       near64:  the per-mesh near tests in f64 (near_box) instead of f32 (near_mesh32), -DRT_NEAR32=0;
       noslots: the default library on a scene loaded without its slot tables (RT_TEST_SLOT_MAX_PID=0, the
-               path a 2^23-node octree takes: the pool kernel's node_kids instance)."""
+               path a 2^23-node octree takes: the pool kernel's node_kids instance);
+      noanc:   the role pool's walkers without their 16-bit LDS ancestor columns, popping through pid_up
+               (RT_TEST_ANC_OFF=1: the path of octrees with more than 65536 parents)."""
     if "default" not in _cull_frames:
         _cull_frames["default"] = _cull_run()
     base = _cull_frames["default"]
@@ -169,6 +171,9 @@ def test_walk_culls_do_not_change_frames(variant):
     if variant == "noslots":
         got = _cull_run(env={"RT_TEST_SLOT_MAX_PID": "0"})
         assert got["flying_unicorn/slots"] == 0 and got["cubes/slots"] == 0
+    elif variant == "noanc":
+        got = _cull_run(env={"RT_TEST_ANC_OFF": "1"})
+        assert got["flying_unicorn/slots"] == 1
     else:
         lib = os.path.join(REPO, "raytracer-server_amd", "lib", "variants", variant + ".so")
         assert os.path.exists(lib), f"{lib} not built (make -C raytracer-server_amd variants)"
