@@ -555,19 +555,27 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
     // t, and the hit triangle as its index within the mesh (flat meshes hold <= kFlatMaxTris). The
     // mirror-bounce state (o, pre-bounce throughput) lives in LDS as in k_megakernel_f64 (LdsCold):
     // 12 VGPRs less at 3 waves/SIMD.
-    __shared__ double s_qo[3 * B], s_qdc[3 * B], s_qds[4 * B];
-    __shared__ double s_rt[kFlatMeshes * B];
-    __shared__ uint8_t s_rp[kFlatMeshes * B];
-    __shared__ uint8_t s_ro[kFlatMeshes * B];
     // Scenes without a mirror object (Cfg::nospec) have no mirror-bounce state: its 12 KB hold a
     // camera-sample buffer instead (as k_megakernel_f64's: the next sample's camera ray and RNG state,
     // computed for many lanes at once in a refill pass rather than by a few lanes per iteration).
-    __shared__ double s_cold[C::nospec ? 1 : 6 * B];
+    // Every per-lane 8-byte column lives in one array (RT_FPOOL_COLS): a lane's column addresses are then
+    // one base plus immediate offsets, instead of a base per array, which the register allocator of the
+    // 4-waves/SIMD instance (128 VGPRs) spilled to scratch and reloaded at each use.
+    constexpr int kColQo = 0, kColQdc = 3, kColQds = 6, kColRt = 10, kColX = kColRt + kFlatMeshes;
+    constexpr int kCols = kColX + (C::nospec ? 5 : 6);  // + camera sample (d, RNG) / mirror state (o, beta)
+    __shared__ double s_cols[kCols * B];
+    double* const s_qo = s_cols + kColQo * B;
+    double* const s_qdc = s_cols + kColQdc * B;
+    double* const s_qds = s_cols + kColQds * B;
+    double* const s_rt = s_cols + kColRt * B;
+    __shared__ uint8_t s_rp[kFlatMeshes * B];
+    __shared__ uint8_t s_ro[kFlatMeshes * B];
+    double* const s_cold = s_cols + kColX * B;  // !nospec: LdsCold's 6 columns (stride 256: B == 256)
     using Cold = std::conditional_t<C::nospec, RegCold, LdsCold>;
     Cold cold{};
     if constexpr (!C::nospec) cold = LdsCold{(LdsD*)s_cold + threadIdx.x};
-    __shared__ double s_nbd[C::nospec ? 3 * B : 1];
-    __shared__ uint64_t s_nbr[C::nospec ? 2 * B : 1];
+    double* const s_nbd = s_cols + kColX * B;
+    uint64_t* const s_nbr = (uint64_t*)(s_cols + (kColX + 3) * B);
     LdsD* nbd = (LdsD*)s_nbd + (C::nospec ? threadIdx.x : 0);
     __attribute__((address_space(3))) uint64_t* nbr = (__attribute__((address_space(3))) uint64_t*)s_nbr + (C::nospec ? threadIdx.x : 0);
     bool nvalid = false;  // nbd / nbr hold sample s + 1 of subpixel id
