@@ -1832,10 +1832,14 @@ RT_DEV double light_pdf_area(const DevScene& sc) { return sc.light_pdf; }
 // Camera ray of server.rs:339-357 for subpixel (sx, sy) of pixel (x, y_ref).
 RT_DEV Ray camera_ray(const DevScene& sc, V3 cx, V3 cy, double w, double h, int x, int y, int sx, int sy, double u1,
                       double u2) {
+    // the tent filter's two square roots, one per branch in the reference, as one sqrt_rn of the selected
+    // radicand per axis (sqrt_rn == sqrt bit for bit; the library form only where a wave holds a 0 or tiny one)
     double r1 = 2. * u1;
-    double dx = r1 < 1. ? sqrt(r1) - 1. : 1. - sqrt(2. - r1);
+    const double q1 = sqrt_rn(r1 < 1. ? r1 : 2. - r1);
+    double dx = r1 < 1. ? q1 - 1. : 1. - q1;
     double r2 = 2. * u2;
-    double dy = r2 < 1. ? sqrt(r2) - 1. : 1. - sqrt(2. - r2);
+    const double q2 = sqrt_rn(r2 < 1. ? r2 : 2. - r2);
+    double dy = r2 < 1. ? q2 - 1. : 1. - q2;
     // w, h are image sizes in [1, 2^32]: the shared-divisor division is exact (qdiv)
     V3 d = cx * (qdiv(((double)sx + 0.5 + dx) / 2. + (double)x, w, rcp_rn(w)) - 0.5) +
            cy * (qdiv(((double)sy + 0.5 + dy) / 2. + (double)y, h, rcp_rn(h)) - 0.5) + ld3(sc.cam_dir);
