@@ -238,36 +238,51 @@ def main():
                                 row_step)
     max_rows = max(partition(r, world, args.height, args.partition)[1] for r in range(world))
     rgb = torch.zeros((max_rows, args.width, 3), dtype=torch.uint8, device="cuda")
-    host = torch.zeros((max_rows, args.width, 3), dtype=torch.uint8).pin_memory()
+    # two pinned host buffers: step k's rows are gathered to rank 0 (gloo, on the host) while step k + 1 renders
+    # (stream order keeps the device buffer's next render behind this step's copy-back); the last step's gather
+    # is inside the timed region, so every timed frame is complete on rank 0 when the clock stops
+    hosts = [torch.zeros((max_rows, args.width, 3), dtype=torch.uint8).pin_memory() for _ in range(2)]
+    host = hosts[0]
     stream = torch.cuda.current_stream()
     gathered = [torch.empty_like(host) for _ in range(world)] if (world > 1 and rank == 0) else None
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     kernel_ms = []
+    pending = [None]  # the host buffer whose gather is still to be done
+    last = [hosts[0]]  # the buffer of the last step (its frame: digest, N = 1)
 
-    def step(timed):
+    def flush():
+        if world > 1 and pending[0] is not None:
+            dist.gather(pending[0], gathered if rank == 0 else None, dst=0)  # host-side gather (gloo)
+        pending[0] = None
+
+    def step(i, timed):
+        buf = hosts[i % 2]
         if timed:
             ev0.record(stream)
         rt_amd.render_device(scene, params, rgb.data_ptr(), None, stream.cuda_stream)
         if timed:
             ev1.record(stream)
-        host.copy_(rgb, non_blocking=True)  # the rank's rows to the host
+        buf.copy_(rgb, non_blocking=True)  # the rank's rows to the host
+        flush()  # the previous step's rows, while this one renders
         stream.synchronize()
         if timed:
             kernel_ms.append(ev0.elapsed_time(ev1))
-        if world > 1:
-            dist.gather(host, gathered if rank == 0 else None, dst=0)  # host-side gather (gloo)
+        pending[0] = buf
+        last[0] = buf
 
     # one untimed stats run: path-vertex count of this exact workload (device counter)
     st = rt_amd.render_device(scene, params, rgb.data_ptr(), None, stream.cuda_stream, stats=True)
-    for _ in range(args.warmup):
-        step(False)
+    for i in range(args.warmup):
+        step(i, False)
+    flush()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    for i in range(args.steps):
+        step(i, True)
+    flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -292,7 +307,7 @@ def main():
         if world > 1:
             frame = assemble([g.numpy() for g in gathered], world, args.height, args.partition)
         else:
-            frame = host[:th].numpy()
+            frame = last[0][:th].numpy()
         digest = hashlib.sha1(np.ascontiguousarray(frame).tobytes()).hexdigest()[:16]
         rank_samples = args.width * th * 4 * (args.spp // 4)
         workload = f"{args.scene} {args.width}x{args.height}x{args.spp}spp{' mis' if args.mis else ''}"
