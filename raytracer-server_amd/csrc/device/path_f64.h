@@ -625,10 +625,14 @@ struct OctWalk {
     // found while the cursor was still busy (nlf < nle), and whether the node walk is exhausted.
     int32_t nlf, nle;
     uint32_t ndone;
-    uint32_t enter;  // slot walk: the root is still to be entered (its octant_mask runs in the first step,
-                     // in the same code as every descent's)
+    uint32_t enter;  // bit 0, slot walk: the root is still to be entered (its octant_mask runs in the first step,
+                     // in the same code as every descent's); bit 1: dir_in_range of the walk's ray (walk_begin)
 };
 
+RT_DEV bool dir_in_range(const Ray& ray) {  // kid_tight_hit's `inr` on all three axes
+    auto inr = [](double d) { return fabs(d) >= 0x1p-900 && fabs(d) <= 0x1p900; };
+    return inr(ray.d.x) && inr(ray.d.y) && inr(ray.d.z);
+}
 // LDS column of a walk's ancestor node ids (walk_node_slots' `anc`)
 typedef __attribute__((address_space(3))) int32_t LdsAncI32;
 typedef __attribute__((address_space(3))) uint16_t LdsAncU16;  // pids < 2^16 (DevScene::n_pid): half the LDS
@@ -676,7 +680,7 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
     w.bt = 0.0;
     w.nlf = w.nle = 0;
     w.ndone = 0;
-    w.enter = 0;
+    w.enter = dir_in_range(ray) ? 2u : 0u;  // bit 1: kid_tight_hit's `inr` on every axis, once per walk
     // the slot walk names parents by their row (pid); a root leaf has none, and its walk never reads `cur`
     // (no children to pick), but cur >= 0 is what marks a walk in progress (pool_round)
     w.cur = Slots ? max(m.root_pid, 0) : m.node_base;
@@ -713,7 +717,7 @@ RT_DEV bool walk_begin(const DevScene& sc, const DevMesh& m, const Ray& ray, con
         w.mx[k] = m.root_box[3 + k];
     }
     if constexpr (Slots) {
-        w.enter = 1;  // the first step enters the root (walk_node_slots)
+        w.enter |= 1u;  // the first step enters the root (walk_node_slots)
     } else {
         walk_enter(sc, ray, inv, w);
     }
@@ -815,14 +819,26 @@ RT_DEV int leaf_tris_loaded(const DevScene& sc, const Ray& ray, OctWalk& w, cons
 // subtree's triangle bounds: the same conservative slab test as near_box. Skipping such a child leaves
 // the walk's result unchanged: the reference would descend, test every triangle below it, find none,
 // and go on with the next child in visiting order.
+// The bound codes decode as base + q * step: rt_api.cpp make_slot keeps the scene's slot tables only when no
+// code was clamped to the 16-bit range, so every decoded bound encloses its subtree's padded triangle bounds.
+// (RT_TIGHT_INF=1: round 4's decode, codes 0 / kTightTop as -inf / +inf, which that guarantee makes dead.)
+#ifndef RT_TIGHT_INF
+#define RT_TIGHT_INF 0
+#endif
+RT_DEV double tight_lo(uint32_t q, double step, double base) {
+    return (RT_TIGHT_INF && q == 0u) ? -INFINITY : fma((double)q, step, base);
+}
+RT_DEV double tight_hi(uint32_t q, double step, double base) {
+    return (RT_TIGHT_INF && q == (uint32_t)kTightTop) ? INFINITY : fma((double)q, step, base);
+}
 RT_DEV bool kid_tight_hit(const DevMesh& m, const int4& ks, const Ray& ray, const RayInv& inv) {
     const double step = m.tight_step;
     double t0 = 0.0, t1 = INFINITY;
     bool keep = true, force = false;
     // one axis of near_box's slab test (branch-free: no private arrays, no early exits)
     auto axis = [&](uint32_t ql, uint32_t qh, double base, double o, double d, double rc) {
-        const double lo = ql == 0u ? -INFINITY : fma((double)ql, step, base);
-        const double hi = qh == (uint32_t)kTightTop ? INFINITY : fma((double)qh, step, base);
+        const double lo = tight_lo(ql, step, base);
+        const double hi = tight_hi(qh, step, base);
         const bool inr = fabs(d) >= 0x1p-900 && fabs(d) <= 0x1p900;
         const bool tiny = fabs(d) < 0x1p-900;
         force |= !inr && !tiny;                      // NaN / huge: do not cull
@@ -848,8 +864,8 @@ RT_DEV bool kid_tight_hit_inr(const DevMesh& m, const int4& ks, const Ray& ray, 
     const double step = m.tight_step;
     double t0 = 0.0, t1 = INFINITY;
     auto axis = [&](uint32_t ql, uint32_t qh, double base, double o, double rc) {
-        const double lo = ql == 0u ? -INFINITY : fma((double)ql, step, base);
-        const double hi = qh == (uint32_t)kTightTop ? INFINITY : fma((double)qh, step, base);
+        const double lo = tight_lo(ql, step, base);
+        const double hi = tight_hi(qh, step, base);
         const double ta = (lo - o) * rc, tb = (hi - o) * rc;
         const double tn = fmin(ta, tb), tf = fmax(ta, tb);
         t0 = fmax(t0, tn - 1e-9 * fabs(tn));
@@ -859,10 +875,6 @@ RT_DEV bool kid_tight_hit_inr(const DevMesh& m, const int4& ks, const Ray& ray, 
     axis((uint32_t)ks.y >> 16, (uint32_t)ks.w & 0xFFFFu, m.tight_base[1], ray.o.y, inv.ry);
     axis((uint32_t)ks.z & 0xFFFFu, (uint32_t)ks.w >> 16, m.tight_base[2], ray.o.z, inv.rz);
     return t0 <= t1;
-}
-RT_DEV bool dir_in_range(const Ray& ray) {  // kid_tight_hit's `inr` on all three axes
-    auto inr = [](double d) { return fabs(d) >= 0x1p-900 && fabs(d) <= 0x1p900; };
-    return inr(ray.d.x) && inr(ray.d.y) && inr(ray.d.z);
 }
 // The slot of child octant oi of node `cur` (one 16-byte load: entry + bounds).
 RT_DEV int4 kid_slot(const DevScene& sc, int32_t cur, uint32_t oi) {
@@ -892,6 +904,33 @@ constexpr int kSlotAncLevels = 9;
 // the ancestor `cur` at level `lv` (its box and its first candidate's slot), 0 = nothing (the root still
 // to be entered, or exhausted). The node state this reads is not touched by the triangle tests, so the
 // node operation after them starts from the same state and uses these values instead of loading.
+// The deepest ancestor level lv < w.depth whose remaining-children mask pm (stk byte lv; level 8 in stk8) is
+// non-zero, pm = 0 if none: branch-free (RT_POP_CLZ: the highest non-zero byte of the live part of stk by a
+// count of leading zeros) instead of a loop over the levels, whose trip count is the largest over the wave's
+// popping lanes. Parents sit at depths 0..8 of a walk (MAX_DEPTH 10), so w.depth <= 9 and lv <= 8.
+#ifndef RT_POP_CLZ
+#define RT_POP_CLZ 1
+#endif
+RT_DEV void pop_level(const OctWalk& w, int& lv, uint32_t& pm) {
+#if RT_POP_CLZ
+    const int d = w.depth;
+    const int nb = min(d, 8);
+    const uint64_t live = nb >= 8 ? w.stk : (w.stk & ((1ull << (8 * nb)) - 1ull));
+    const int hb = 63 - __clzll((long long)(live | 1ull));  // (| 1: defined for live == 0, then byte 0 below)
+    const int lb = hb >> 3;
+    const uint32_t pb = (uint32_t)(live >> (8 * lb)) & 0xFFu;
+    const bool at8 = d > 8 && w.stk8 != 0u;
+    lv = at8 ? 8 : lb;
+    pm = at8 ? w.stk8 : pb;
+#else
+    lv = w.depth;
+    pm = 0;
+    while (pm == 0 && lv > 0) {
+        --lv;
+        pm = lv < 8 ? (uint32_t)(w.stk >> (8 * lv)) & 0xFFu : w.stk8;
+    }
+#endif
+}
 struct SlotPF {
     int4 ks;
     double2 b0, b1, b2;
@@ -902,7 +941,7 @@ struct SlotPF {
 template <int AS = 256, class Anc = LdsAncI32>
 RT_DEV void slot_prefetch(const DevScene& sc, const OctWalk& w, const Anc* anc, SlotPF& pf) {
     pf.kind = 0;
-    if (w.enter) return;
+    if (w.enter & 1u) return;
     uint32_t pm = w.pm;
     int32_t cur = w.cur;
     if (pm == 0) {
@@ -935,8 +974,8 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
                            Anc* anc = nullptr, const SlotPF* pf = nullptr) {
     RT_DBG_TSTART(t_pop);
     uint32_t exist = 0;  // a node to enter: its existence mask (the root at a walk's start, or a descent)
-    if (w.enter) {
-        w.enter = 0;
+    if (w.enter & 1u) {
+        w.enter &= ~1u;
         exist = (uint32_t)m.root_exist;
     } else {
     if (pf && pf->kind == 2) {  // the pop, its box fetched ahead (slot_prefetch)
@@ -947,12 +986,9 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
         w.mn[0] = pf->b0.x; w.mn[1] = pf->b0.y; w.mn[2] = pf->b1.x;
         w.mx[0] = pf->b1.y; w.mx[1] = pf->b2.x; w.mx[2] = pf->b2.y;
     } else if (w.pm == 0) {  // `cur` exhausted: resume at the nearest ancestor with children left
-        int lv = w.depth;
-        uint32_t pm = 0;
-        while (pm == 0 && lv > 0) {
-            --lv;
-            pm = lv < 8 ? (uint32_t)(w.stk >> (8 * lv)) & 0xFFu : w.stk8;
-        }
+        int lv;
+        uint32_t pm;
+        pop_level(w, lv, pm);
         if (pm == 0) {  // the root is exhausted
             RT_DBG_TEND(13, t_pop);
             return WALK_MISS;
@@ -997,7 +1033,8 @@ RT_DEV int walk_node_slots(const DevScene& sc, const DevMesh& m, const Ray& ray,
     // picks per step (a culled pick is as if the reference found nothing below that child)
     int32_t c = kKidEmpty;
     uint32_t oi = 0;
-    const bool inr = RT_TIGHT_FAST && wave_all(dir_in_range(ray));  // wave-uniform: one form of the test per step
+    // wave-uniform: one form of the test per step (each lane's dir_in_range from its walk's start, OctWalk::enter)
+    const bool inr = RT_TIGHT_FAST && wave_all((w.enter & 2u) != 0u);
     auto tight = [&](const int4& ks) { return inr ? kid_tight_hit_inr(m, ks, ray, inv) : kid_tight_hit(m, ks, ray, inv); };
 #if RT_SLOT_PAIR
     if (!pf) {

@@ -94,7 +94,8 @@ RT_LAYOUT_FN int32_t kid_leaf(int32_t leaf, int32_t first, int32_t count) {
 // with the parent encoding below) and the child subtree's triangle
 // bounds ("tight box": the vertices of every triangle in the subtree's leaves, padded by
 // DevMesh::cull_pad), rounded OUTWARD to 16-bit codes over the mesh's range (DevMesh::tight_base /
-// tight_step: bound = base + q * step, one extra step each way; a low code 0 means -inf, a high code
+// tight_step: bound = base + q * step, one extra step each way (rt_api.cpp make_slot: no code is clamped, or the
+// scene has no slot tables; before round 5 a low code 0 meant -inf, a high code
 // 65535 +inf). Triangles may reach far outside their octant (geometry.rs:1038-1060 assigns any
 // triangle that touches it), so the bounds are not the octant box. A ray that passes farther than the
 // padding from them cannot get tri_intersect == true from any triangle below, so the reference's walk

@@ -117,7 +117,7 @@ RT_DEV void park_load(const Park& p, WalkRegs& r) {
     r.w.bt = p.D(15);
     r.wt = p.D(16);
     r.w.cur = p.I(0); r.w.depth = p.I(1) & 0xFF; r.w.ndone = ((uint32_t)p.I(1) >> 24) & 1u;
-    r.w.enter = ((uint32_t)p.I(1) >> 25) & 1u; r.w.path = (uint32_t)p.I(2);
+    r.w.enter = ((uint32_t)p.I(1) >> 25) & 3u; r.w.path = (uint32_t)p.I(2);
     r.w.pm = (uint32_t)p.I(3);
     r.w.stk = (uint64_t)(uint32_t)p.I(4) | ((uint64_t)(uint32_t)p.I(5) << 32); r.w.stk8 = (uint32_t)p.I(6);
     r.w.order = (uint32_t)p.I(7); r.w.lpos = p.I(8); r.w.lend = p.I(9); r.w.best = p.I(10);
@@ -354,7 +354,7 @@ RT_DEV void park2_load(const Park2& p, WalkRegs& r) {
     r.w.cur = p.I(0);
     const uint32_t dps = (uint32_t)p.I(1);
     r.w.depth = (int32_t)(dps & 0xFFu); r.w.pm = (dps >> 8) & 0xFFu; r.w.stk8 = (dps >> 16) & 0xFFu;
-    r.w.ndone = (dps >> 24) & 1u; r.w.enter = (dps >> 25) & 1u;
+    r.w.ndone = (dps >> 24) & 1u; r.w.enter = (dps >> 25) & 3u;
     r.w.path = (uint32_t)p.I(2);
     r.w.stk = (uint64_t)(uint32_t)p.I(3) | ((uint64_t)(uint32_t)p.I(4) << 32);
     r.w.order = (uint32_t)p.I(5); r.w.lpos = p.I(6); r.w.lend = p.I(7); r.w.best = p.I(8);

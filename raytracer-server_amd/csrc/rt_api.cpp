@@ -65,15 +65,25 @@ struct Packed {
 // A child slot (scene_layout.h KidSlot): the child entry and its subtree's triangle bounds b (lo xyz,
 // hi xyz, already padded), rounded OUTWARD to 16-bit codes over the mesh's range (base + q * step), one
 // extra step each way so that device-side rounding of the dequantised bounds cannot move them inward.
-rt::KidSlot make_slot(int32_t kid, const rt::DevMesh& dm, const double* b) {
+// The device decodes every code as base + q * step (path_f64.h kid_tight_hit), so a bound is conservative
+// only if its code was not clamped to the range: for a mesh of extent E > 0 the codes of its padded
+// triangle bounds lie in about [E / step, 2 E / step] = [21845, 43690], but a mesh whose cull padding
+// exceeds E (a sub-1e-7 mesh far from the origin) would clamp. *exact turns false then, and the scene
+// walks without slot tables (node_kids: the same result without the subtree culls).
+rt::KidSlot make_slot(int32_t kid, const rt::DevMesh& dm, const double* b, bool* exact) {
     rt::KidSlot s{};
     s.kid = kid;
     for (int k = 0; k < 3; ++k) {
         s.lo[k] = 0;
         s.hi[k] = (uint16_t)rt::kTightTop;
-        if (kid == rt::kKidEmpty || !(dm.tight_step > 0.0) || !std::isfinite(dm.tight_step)) continue;
+        if (kid == rt::kKidEmpty) continue;  // never picked: its slot is not read
+        if (!(dm.tight_step > 0.0) || !std::isfinite(dm.tight_step)) {
+            *exact = false;
+            continue;
+        }
         const double ql = std::floor((b[k] - dm.tight_base[k]) / dm.tight_step) - 1.0;
         const double qh = std::ceil((b[3 + k] - dm.tight_base[k]) / dm.tight_step) + 1.0;
+        if (!(ql >= 1.0 && qh <= (double)(rt::kTightTop - 1))) *exact = false;
         s.lo[k] = ql >= 1.0 ? (uint16_t)std::min(ql, (double)(rt::kTightTop - 1)) : (uint16_t)0;
         s.hi[k] = qh <= (double)(rt::kTightTop - 1) ? (uint16_t)std::max(qh, 1.0) : (uint16_t)rt::kTightTop;
     }
@@ -485,7 +495,9 @@ int pack_scene(rt_scene* s) {
                         for (int q = 0; q < 8; ++q) ex |= (oc.child[8 * (size_t)c8 + q] >= 0 ? 1u : 0u) << q;
                         e = rt::slot_parent(e, ex);
                     }
-                    p.slots.push_back(make_slot(e, dm, b));
+                    bool exact = true;
+                    p.slots.push_back(make_slot(e, dm, b, &exact));
+                    if (!exact) slots_ok = false;  // a clamped bound code: no slot tables (make_slot)
                 }
             }
         }
