@@ -831,6 +831,21 @@ RT_DEV double tight_lo(uint32_t q, double step, double base) {
 RT_DEV double tight_hi(uint32_t q, double step, double base) {
     return (RT_TIGHT_INF && q == (uint32_t)kTightTop) ? INFINITY : fma((double)q, step, base);
 }
+// The slab test's final comparison with its 1e-9 relative padding. RT_TIGHT_PAD1: the padding applied once, to
+// the interval ends t0 = max(0, tn_k), t1 = min(inf, tf_k), instead of to every axis' tn_k / tf_k before the max /
+// min: x -> RN(x - RN(1e-9 |x|)) and x -> RN(x + RN(1e-9 |x|)) are non-decreasing in x (between adjacent doubles x
+// moves by an ulp, the padding by 1e-9 of that), so they commute with max and min (and map 0 to 0, inf to inf),
+// and the comparison is the per-axis form's, bit for bit, with 4 VALU instead of 12.
+#ifndef RT_TIGHT_PAD1
+#define RT_TIGHT_PAD1 1
+#endif
+RT_DEV bool tight_padded_le(double t0, double t1) {
+#if RT_TIGHT_PAD1
+    return t0 - 1e-9 * fabs(t0) <= t1 + 1e-9 * fabs(t1);
+#else
+    return t0 <= t1;
+#endif
+}
 RT_DEV bool kid_tight_hit(const DevMesh& m, const int4& ks, const Ray& ray, const RayInv& inv) {
     const double step = m.tight_step;
     double t0 = 0.0, t1 = INFINITY;
@@ -845,13 +860,18 @@ RT_DEV bool kid_tight_hit(const DevMesh& m, const int4& ks, const Ray& ray, cons
         keep &= !tiny || (o >= lo && o <= hi);       // (nearly) parallel slab: origin must lie inside it
         const double ta = (lo - o) * rc, tb = (hi - o) * rc;
         const double tn = fmin(ta, tb), tf = fmax(ta, tb);
+#if RT_TIGHT_PAD1
+        t0 = inr ? fmax(t0, tn) : t0;
+        t1 = inr ? fmin(t1, tf) : t1;
+#else
         t0 = inr ? fmax(t0, tn - 1e-9 * fabs(tn)) : t0;
         t1 = inr ? fmin(t1, tf + 1e-9 * fabs(tf)) : t1;
+#endif
     };
     axis((uint32_t)ks.y & 0xFFFFu, (uint32_t)ks.z >> 16, m.tight_base[0], ray.o.x, ray.d.x, inv.rx);
     axis((uint32_t)ks.y >> 16, (uint32_t)ks.w & 0xFFFFu, m.tight_base[1], ray.o.y, ray.d.y, inv.ry);
     axis((uint32_t)ks.z & 0xFFFFu, (uint32_t)ks.w >> 16, m.tight_base[2], ray.o.z, ray.d.z, inv.rz);
-    return force || (keep && t0 <= t1);
+    return force || (keep && tight_padded_le(t0, t1));
 }
 // kid_tight_hit for rays whose direction components all lie in [2^-900, 2^900] in magnitude (every ray of
 // the wave: walk_node_slots' wave vote), where its `inr` holds on every axis, so `force` and `keep` keep
@@ -868,13 +888,18 @@ RT_DEV bool kid_tight_hit_inr(const DevMesh& m, const int4& ks, const Ray& ray, 
         const double hi = tight_hi(qh, step, base);
         const double ta = (lo - o) * rc, tb = (hi - o) * rc;
         const double tn = fmin(ta, tb), tf = fmax(ta, tb);
+#if RT_TIGHT_PAD1
+        t0 = fmax(t0, tn);
+        t1 = fmin(t1, tf);
+#else
         t0 = fmax(t0, tn - 1e-9 * fabs(tn));
         t1 = fmin(t1, tf + 1e-9 * fabs(tf));
+#endif
     };
     axis((uint32_t)ks.y & 0xFFFFu, (uint32_t)ks.z >> 16, m.tight_base[0], ray.o.x, inv.rx);
     axis((uint32_t)ks.y >> 16, (uint32_t)ks.w & 0xFFFFu, m.tight_base[1], ray.o.y, inv.ry);
     axis((uint32_t)ks.z & 0xFFFFu, (uint32_t)ks.w >> 16, m.tight_base[2], ray.o.z, inv.rz);
-    return t0 <= t1;
+    return tight_padded_le(t0, t1);
 }
 // The slot of child octant oi of node `cur` (one 16-byte load: entry + bounds).
 RT_DEV int4 kid_slot(const DevScene& sc, int32_t cur, uint32_t oi) {
