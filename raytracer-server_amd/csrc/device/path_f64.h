@@ -658,8 +658,9 @@ RT_DEV void walk_enter_mask(const Ray& ray, const RayInv& inv, OctWalk& w, uint3
     RT_DBG(2);
     const uint32_t m = octant_mask(w.mn, w.mx, ray, inv) & exist;
     uint32_t pm = 0;
+    // bit q of pm = bit order[q] of m: one bit-field extract at a variable offset and one shift-or per rank
 #pragma unroll
-    for (int q = 0; q < 8; ++q) pm |= ((m >> ((w.order >> (4 * q)) & 0xF)) & 1u) << q;
+    for (int q = 0; q < 8; ++q) pm |= __builtin_amdgcn_ubfe(m, (w.order >> (4 * q)) & 0xFu, 1u) << q;
     w.pm = pm;
 }
 
