@@ -335,6 +335,9 @@ RT_DEV V3 tri_normal(const TR& tr) {
         return v3(cr.x / mg, cr.y / mg, cr.z / mg);
     }
 }
+#ifndef RT_TRI_MINORS
+#define RT_TRI_MINORS 1  // tri_t's determinants through their shared minors (1), or four det3 calls (0: A/B)
+#endif
 template <class TR>
 RT_DEV bool tri_t(const TR& tr, const Ray& ray, double* tout) {
     V3 n = tri_normal(tr);
@@ -342,8 +345,20 @@ RT_DEV bool tri_t(const TR& tr, const Ray& ray, double* tout) {
     V3 ab = ld3(tr.ab), ac = ld3(tr.ac);
     V3 b = ray.o - ld3(tr.a);
     V3 nd = -ray.d;
+#if RT_TRI_MINORS
+    // det3's cofactor expansion of the four determinants with their seven distinct 2x2 minors computed once
+    // (each det3(v0, v1, v2) = v0.x M1 - v1.x M2 + v2.x M3 with the same minors, the same operations)
+    const double mA = ab.y * ac.z - ab.z * ac.y, mB = nd.y * ac.z - nd.z * ac.y, mC = nd.y * ab.z - nd.z * ab.y;
+    const double mD = b.y * ac.z - b.z * ac.y, mE = b.y * ab.z - b.z * ab.y, mF = nd.y * b.z - nd.z * b.y;
+    const double mG = ab.y * b.z - ab.z * b.y;
+    double det = nd.x * mA - ab.x * mB + ac.x * mC;  // det3(nd, ab, ac)
+    double tn = b.x * mA - ab.x * mD + ac.x * mE;    // det3(b, ab, ac)
+    double un = nd.x * mD - b.x * mB + ac.x * mF;    // det3(nd, b, ac)
+    double vn = nd.x * mG - ab.x * mF + b.x * mC;    // det3(nd, ab, b)
+#else
     double det = det3(nd, ab, ac);
     double tn = det3(b, ab, ac), un = det3(nd, b, ac), vn = det3(nd, ab, b);
+#endif
     double t, u, v;
     if (wave_all(rcp_safe(det))) {  // wave-uniform
         double y = rcp_rn(det);
