@@ -152,6 +152,9 @@ typedef const __attribute__((address_space(4))) DevTri CTri;
 // lists are in triangle order, so the earlier hit is the lower index: the walk's strict <). Same
 // bits as flat_query_leaves, without its per-leaf best-hit updates (8 leaves x 4 VALU per triangle).
 // The ray reciprocals are taken only for lanes whose ray hits a triangle (the leaf boxes' test).
+#ifndef RT_FLAT_GRID_ORDER
+#define RT_FLAT_GRID_ORDER 1  // the winning leaf by root_order_grid's order (1) or first_visited's argmin (0: A/B)
+#endif
 RT_DEV bool flat_query(const DevScene& sc, int mi, const Ray& ray, double* t_out, int* prim_out) {
     CMesh* M = (CMesh*)(uintptr_t)(sc.meshes + mi);
     const int n = M->n_tris, base = M->tri_base;
@@ -189,7 +192,24 @@ RT_DEV bool flat_query(const DevScene& sc, int mi, const Ray& ray, double* t_out
 #pragma unroll
             for (int k = 0; k < 6; ++k) rb[k] = M->root_box[k];
             cand &= octant_mask(rb, rb + 3, ray, make_inv(ray.d));  // the children's box_hit, bit i = octant i
-            if (cand) win = first_visited(*M, ray, cand);
+            if (cand) {
+#if RT_FLAT_GRID_ORDER
+                // the whole visiting order from the octant centres' grid (path_f64.h root_order_grid: root_order's
+                // result whenever no two radicands are near a tie), its first candidate; else first_visited
+                uint32_t order;
+                if (wave_all(root_order_grid(*M, ray, &order))) {
+#pragma unroll
+                    for (int q = 7; q >= 0; --q) {
+                        const uint32_t oi = (order >> (4 * q)) & 0xFu;
+                        win = ((cand >> oi) & 1u) ? (int)oi : win;
+                    }
+                } else {
+                    win = first_visited(*M, ray, cand);
+                }
+#else
+                win = first_visited(*M, ray, cand);
+#endif
+            }
         }
     }
     if (win < 0) return false;
