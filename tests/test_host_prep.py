@@ -331,3 +331,63 @@ def test_root_order_grid_form_matches_insertion_sort():
             claimed[mode] += 1
             assert order == reference(cs, o), (o, order, reference(cs, o))
     assert claimed[0] > 0.999 * 15000 and claimed[3] > 0.99 * 15000  # random origins: the fast form almost always
+
+
+def _speck_toml(tmp_path, n=64):
+    """A mesh far smaller than its own cull padding: n triangles inside a 1e-8 cube at (1e6, 1e6, 1e6), whose
+    cull padding is 1e-7 * 1e6 = 0.1 (rt_api.cpp pack_scene)."""
+    rng = np.random.default_rng(3)
+    lines = []
+    for t in range(n):
+        for _ in range(3):
+            x, y, z = (1e6 + int(k) * 1e-9 for k in rng.integers(0, 10, 3))
+            lines.append(f"v {x!r} {y!r} {z!r}")
+        lines.append(f"f {3 * t + 1} {3 * t + 2} {3 * t + 3}")
+    (tmp_path / "speck.obj").write_text("\n".join(lines) + "\n")
+    text = """
+[camera]
+pos = [50.0, 52.0, 295.6]
+dir = [0.0, -0.042612, -1.0]
+[[objects]]
+brdf = { type = "diffuse", kd = [0.9, 0.9, 0.9] }
+geometry = { type = "mesh", path = "speck.obj" }
+[[objects]]
+emitted = [50.0, 50.0, 50.0]
+brdf = { type = "diffuse", kd = [0.0, 0.0, 0.0] }
+geometry = { type = "sphere", pos = [50.0, 70.0, 100.0], r = 4.0 }
+"""
+    return _write(tmp_path, text)
+
+
+def test_slot_bound_codes_never_clamp_on_reference_meshes(rt, tmp_path):
+    """rt_api.cpp make_slot: the walks decode every subtree-bound code as base + q * step (path_f64.h
+    tight_lo / tight_hi), which encloses the subtree only if no code was clamped to the 16-bit range, so a
+    scene keeps its slot tables only then. The reference meshes keep them (their codes lie in about
+    [E / step, 2 E / step]); a mesh smaller than its own cull padding (1e-7 of its coordinates' scale), far
+    from the origin, clamps and is walked through the plain child tables (the same result without the
+    subtree culls)."""
+    for name in ("flying_unicorn", "cubes"):
+        assert rt.Scene.from_toml(scene_path(name)).info()["slot_tables"] == 1, name
+    speck = rt.Scene.from_toml(_speck_toml(tmp_path), str(tmp_path)).info()
+    assert speck["parents"] > 0  # an octree with slot rows to encode
+    assert speck["slot_tables"] == 0
+
+
+def test_tight_padding_commutes_with_max_min():
+    """path_f64.h tight_padded_le: the slab test pads the interval ends once, f(max tn) <= g(min tf) with
+    f(x) = x - 1e-9|x|, g(x) = x + 1e-9|x| in f64, instead of max f(tn) <= min g(tf) per axis. f and g are
+    non-decreasing in IEEE f64 (checked here on adjacent doubles, signed zeros and a spread of magnitudes),
+    so they commute with max / min and the two forms decide every test alike (checked on random slabs)."""
+    rng = np.random.default_rng(7)
+    f = lambda x: x - 1e-9 * np.abs(x)  # noqa: E731
+    g = lambda x: x + 1e-9 * np.abs(x)  # noqa: E731
+    x = np.concatenate([rng.standard_normal(200000) * 10.0 ** rng.integers(-300, 300, 200000),
+                        np.array([0.0, -0.0, 5e-324, -5e-324, 1e308, -1e308])])
+    x.sort()
+    up = np.nextafter(x, np.inf)
+    assert np.all(f(up) >= f(x)) and np.all(g(up) >= g(x))
+    tn = rng.standard_normal((100000, 3)) * 10.0 ** rng.integers(-5, 8, (100000, 1))
+    tf = tn + np.abs(rng.standard_normal((100000, 3))) * 10.0 ** rng.integers(-12, 3, (100000, 1))
+    t0, t1 = np.maximum(0.0, tn.max(axis=1)), tf.min(axis=1)
+    per_axis = np.maximum(0.0, f(tn).max(axis=1)) <= np.minimum(np.inf, g(tf).min(axis=1))
+    assert np.array_equal(per_axis, f(t0) <= g(t1))
