@@ -234,8 +234,9 @@ static inline int env_int(const char* name, int dflt) {
 #endif
 // Split tail (RenderArgs::n_whole): the last subpixels are handed out in chunks of samples, so the
 // frame does not end with lanes idling while others finish a whole subpixel (the 1/N-sized frames
-// of an N-GPU run hold only a few subpixels per lane). Up to one subpixel per resident lane is
-// split, limited by the scratch buffer (tail_cap bytes); RT_MK_TAIL=0 disables it.
+// of an N-GPU run hold only a few subpixels per lane). plan_tail's split_x2 / 2 subpixels per resident
+// lane are split, at most nsub / cap_div, limited by the scratch buffer (tail_cap bytes); RT_MK_TAIL=0
+// disables it.
 // Runs of whole subpixels per ticket: about RT_MK_UNIT_SAMPLES (256) samples per ticket, but at least
 // RT_MK_UNITS_PER_LANE (16) runs per resident lane, so the frame's end stays balanced (2 runs per lane
 // left the unicorn's lanes idling behind a few long runs: -30%). At 1024 spp that is one subpixel per
@@ -250,26 +251,37 @@ static inline void plan_units(RenderArgs& a, long lanes) {
     a.n_wunits = (int32_t)(((long)a.n_whole + b - 1) / b);
 }
 
-static inline void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_buf, size_t tail_cap) {
+// split_x2 = 1 (half a subpixel per lane, cap_div 2: at most half the frame): the analytic and flat-mesh
+// kernels, whose subpixels cost about the same, so two chunks per lane at the frame's end balance it
+// (one subpixel per lane measured no better, profiles/r05ae_tail_probe_cornell1024.log). The mesh walk
+// kernels pass 12 and 1 (six subpixels per path slot, up to the whole frame): a unicorn subpixel's cost
+// depends on where it lies (walls or the mesh), and the last whole subpixels' spread left an N = 8 share
+// at 0.81 of the full frame's rate with half a subpixel per slot, 0.96 with six (profiles/r05bc_tail.log).
+static inline void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_buf, size_t tail_cap, int split_x2 = 1,
+                             int cap_div = 2) {
     static const int tail_env = env_int("RT_MK_TAIL", 1);
-    // split subpixels per resident lane, as 1 / RT_MK_TAIL_DIV (2: half a subpixel per lane, i.e. two chunks
-    // per lane at the frame's end, which keeps the end as balanced as one subpixel per lane did while the
-    // scratch traffic halves; 1 = round 4's one subpixel per lane)
-    static const int tail_div = std::max(1, env_int("RT_MK_TAIL_DIV", 2));
-    // chunks of 2^chunk_lg samples, about RT_MK_TAIL_CPS (4) per subpixel: every chunk costs a
-    // ticket on the one global counter, and short chunks make those atomics the bottleneck of the
-    // tail (16 per subpixel measured 11% slower on the whole frame)
-    // ... and at least 32 samples (≈500 wave iterations): shorter chunks turn over so often that the
-    // counter's atomics saturate (8-sample chunks at 256 spp: the tail ran at a third of the speed)
-    static const int cps_target = std::max(1, env_int("RT_MK_TAIL_CPS", 4));
-    a.chunk_lg = 5;
+    // A/B overrides: RT_MK_TAIL_MUL / RT_MK_TAIL_DIV subpixels per lane (defaults 1 / 2 once either is set),
+    // RT_MK_TAIL_CAP_DIV, RT_MK_TAIL_MIN_LG (the shortest chunk, 2^min_lg samples)
+    static const int env_mul = env_int("RT_MK_TAIL_MUL", 0), env_div = env_int("RT_MK_TAIL_DIV", 0);
+    static const int env_cap = env_int("RT_MK_TAIL_CAP_DIV", 0);
+    static const int min_lg = std::max(2, env_int("RT_MK_TAIL_MIN_LG", 5));
+    const long split_want = (env_mul > 0 || env_div > 0)
+                                ? lanes * std::max(1, env_mul) / (env_div > 0 ? env_div : 2)
+                                : lanes * std::max(1, split_x2) / 2;
+    if (env_cap > 0) cap_div = env_cap;
+    // chunks of 2^chunk_lg samples, about RT_MK_TAIL_CPS (8) per subpixel, and at least 32 samples: every
+    // chunk costs a ticket on the one global counter, whose device-scope atomics saturate when chunks turn
+    // over faster (16-sample chunks: the cornell frame +1.9%, 8-sample: +5%, profiles/r05az_tail.log); 8
+    // per subpixel (4 until round 5) gave an N = 8 cornell share 0.933 -> 0.939 of the full frame's rate
+    static const int cps_target = std::max(1, env_int("RT_MK_TAIL_CPS", 8));
+    a.chunk_lg = min_lg;
     while ((a.n_samples >> a.chunk_lg) > cps_target) ++a.chunk_lg;
     a.tail_cps = (a.n_samples + (1 << a.chunk_lg) - 1) >> a.chunk_lg;
     // chunk 0 of a split subpixel sums in place (tail_stores): scratch only for the samples after it
     const size_t per_sub = (size_t)std::max(0, a.n_samples - (1 << a.chunk_lg)) * 3 * sizeof(double);
     long n_split = 0;
     if (tail_env && tail_buf && a.n_samples >= 64 && a.tail_cps >= 2 && per_sub > 0)
-        n_split = std::min({lanes / tail_div, nsub / 2, (long)(tail_cap / per_sub)});
+        n_split = std::min({split_want, nsub / std::max(1, cap_div), (long)(tail_cap / per_sub)});
     a.n_whole = (int32_t)(nsub - n_split);
     a.tail_buf = tail_buf;
     plan_units(a, lanes);

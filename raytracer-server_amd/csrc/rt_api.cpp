@@ -1064,15 +1064,17 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
         if (e == hipSuccess) {
             a.counters = ps ? ws->counters : nullptr;
             // split-tail scratch (megakernel_common.h plan_tail): the samples after chunk 0 of the subpixels a
-            // launch splits — half a subpixel per resident lane, and no f64 megakernel holds more than 1024
-            // lanes per CU (4 waves/SIMD; the 1024-thread query pool; the role pool's <= 1024 paths), so
-            // 512 per CU (2^17 on 256 CUs: 604 MB at 1024 spp), at most 1.5 GB. A smaller buffer only
-            // splits fewer subpixels (plan_tail), with the same frame bits.
+            // launch splits — half a subpixel per resident lane in the analytic and flat-mesh kernels (no more
+            // than 1024 lanes per CU: 4 waves/SIMD, the 1024-thread query pool), so 512 per CU (2^17 on 256
+            // CUs: 704 MB at 1024 spp); six per path slot in the mesh walk kernels (<= 1024 slots per CU) —
+            // at most 1.5 GB. A smaller buffer only splits fewer subpixels (plan_tail), with the same frame bits.
+            const bool walk = (a.features & 1) && !a.all_flat;
             int dev = 0, ncu = 256;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
             const size_t per_sub = rt::tail_scratch_per_subpixel(a.n_samples);
-            const size_t want = std::min<size_t>((size_t)3 << 29, per_sub * std::min<size_t>(npix * 4 / 2, (size_t)std::max(ncu, 1) * 512));
+            const size_t per_cu = walk ? 6 * 1024 : 512;
+            const size_t want = std::min<size_t>((size_t)3 << 29, per_sub * std::min<size_t>(npix * 4, (size_t)std::max(ncu, 1) * per_cu));
             if (!fp32 && per_sub > 0 && want >= per_sub) {
                 if (ws->ensure_tail(want) != hipSuccess) (void)hipGetLastError();  // no tail split then
             }
