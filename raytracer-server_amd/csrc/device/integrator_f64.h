@@ -30,11 +30,15 @@
 #ifndef RT_OPT_RR
 #define RT_OPT_RR 1    // Russian roulette as an integer comparison of the draw (Rng::below53)
 #endif
+#ifndef RT_OPT_BETA
+#define RT_OPT_BETA 1  // continuation weight f cos / (pdf p) as k / p (diffuse and mirror vertices)
+#endif
 
 namespace rt {
 namespace f64 {
 
 enum : int { K_CAMERA = 0, K_SPEC = 1, K_DIFF = 2 };
+constexpr double kInvSurvival = 1.0 / SURVIVAL_PROBABILITY;
 
 struct PathState {
     Ray ray;
@@ -299,12 +303,25 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
     RT_DBG_TEND(11, t_bs);
     ps.r0 = rng.s0;
     ps.r1 = rng.s1;
-    V3 f = brdf_eval<C>(obj, nrm, o, wi);
     if (spec) {  // Le(x') after a mirror bounce is weighted by the beta before it; o goes on unchanged
         cold.set_bemit(ps, ps.beta);
         cold.set_o(ps, o);
     }
+#if RT_OPT_BETA
+    // f cos / (pdf p) with cos and pdf cancelled: diffuse f = kd / pi, pdf = cos / pi (scene.rs:41-43,
+    // 56-70); mirror f = ks / cos (wi is exactly flip_across(o, n), so Specular::eval's equal_within
+    // holds), pdf = 1 (scene.rs:44-55, 71-74) — both k / p. Same value up to the last bits; cos == 0
+    // (the reference's 0 / 0) and Phong take the general form.
+    const double cw = dot(nrm, wi);
+    if ((!C::phong || obj.brdf != BRDF_PHONG) && cw != 0.0) {
+        ps.beta = mult(ps.beta, ld3(obj.k)) * (ps.depth <= (uint32_t)MAX_BOUNCES ? 1.0 : kInvSurvival);
+    } else {
+        ps.beta = mult(ps.beta, brdf_eval<C>(obj, nrm, o, wi)) * cw / (pdf * p);
+    }
+#else
+    V3 f = brdf_eval<C>(obj, nrm, o, wi);
     ps.beta = mult(ps.beta, f) * dot(nrm, wi) / (pdf * p);
+#endif
     ps.ray = Ray{x, wi};
     ps.kind = spec ? K_SPEC : K_DIFF;
     ps.pdf_prev = use_mis ? pdf : 0.0;
