@@ -30,6 +30,9 @@
 #ifndef RT_OPT_RR
 #define RT_OPT_RR 1    // Russian roulette as an integer comparison of the draw (Rng::below53)
 #endif
+#ifndef RT_OPT_NEE
+#define RT_OPT_NEE 1   // the NEE term's scalar factors through one reciprocal (MIS: the weight cancelled)
+#endif
 #ifndef RT_OPT_BETA
 #define RT_OPT_BETA 1  // continuation weight f cos / (pdf p) as k / p (diffuse and mirror vertices)
 #endif
@@ -181,8 +184,15 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
     } else if (C::mis && hr.obj == sc.light && ps.pdf_prev > 0.0) {
         // MIS, BSDF strategy: emitted radiance with the balance-heuristic weight
         double cosl = dot(nrm, -ps.ray.d);
+#if RT_OPT_NEE
+        // pdf_prev / (pdf_prev + pdf_l) with pdf_l = pdfA t^2 / cosl: numerator and denominator times cosl
+        // (one division; cosl == 0 gives 0 like the reference's pdf_l = inf)
+        const double pc = ps.pdf_prev * cosl;
+        double wgt = pc / (pc + light_pdf_area(sc) * (hr.t * hr.t));
+#else
         double pdf_l = light_pdf_area(sc) * (hr.t * hr.t) / cosl;
         double wgt = ps.pdf_prev / (ps.pdf_prev + pdf_l);
+#endif
         ps.L = ps.L + mult(ps.beta, ld3(obj.emitted) * wgt);
     }
     V3 o = -ps.ray.d;  // the out direction, except after a mirror bounce (which keeps the previous one)
@@ -276,13 +286,23 @@ RT_DEV bool shade_vertex(const DevScene& sc, const RenderArgs& a, PathState& ps,
             }
             V3 c;
             if (!use_mis) {
+#if RT_OPT_NEE
+                // one scalar weight, one reciprocal (magnitude only: the same value up to the last bits)
+                c = lef * (vis * dot(nrm, i) * dot(ny, -i) * rcp_any(r_sqr * pdfA));
+#else
                 c = lef * vis * dot(nrm, i) * dot(ny, -i) / (r_sqr * pdfA);
+#endif
             } else {
                 double cosl = dot(ny, -i);
                 double pdf_l = pdfA * r_sqr / cosl;
                 double pdf_b = dot(nrm, i) * FRAC_1_PI;
                 c = v3(0, 0, 0);
+#if RT_OPT_NEE
+                // (pdf_l / (pdf_l + pdf_b)) / pdf_l == 1 / (pdf_l + pdf_b)
+                if (vis > 0. && cosl > 0. && pdf_b > 0.) c = lef * (dot(nrm, i) * rcp_any(pdf_l + pdf_b));
+#else
                 if (vis > 0. && cosl > 0. && pdf_b > 0.) c = lef * dot(nrm, i) * ((pdf_l / (pdf_l + pdf_b)) / pdf_l);
+#endif
             }
             if (defer && defer->pending) defer->c = mult(ps.beta, c);  // added later iff no mesh occludes
             else ps.L = ps.L + mult(ps.beta, c);

@@ -62,6 +62,11 @@ RT_DEV double rcp_rn(double b) {
     e = fma(-b, r, 1.0);
     return fma(e, r, r);
 }
+// 1 / b for any b: rcp_rn's sequence when every lane of the wave is in its range, else the library's
+RT_DEV double rcp_any(double b) {
+    if (wave_all(rcp_safe(b))) return rcp_rn(b);
+    return 1.0 / b;
+}
 #ifndef RT_OPT_QDIV
 #define RT_OPT_QDIV 1  // A/B: sign of a zero quotient by copysign (1) or by a select on r == 0 (0)
 #endif
