@@ -10,26 +10,31 @@ RCCL collective is on the data path (north_star: "tiles gathered on the host"). 
 fixed: scaling = "strong". Rank 0 prints one JSON line.
 
 roofline (dominant kernel = the render megakernel; kernel_ms = its average device time per launch,
-HIP events recorded on the stream the kernel runs on):
-  * bound "hbm": achieved / peak / frac are SURVEY §8(d)'s HBM roofline model, the figure §8(d) names
-    for roofline.achieved (what limits the megakernel itself is in `binds` and `compute` below):
-    88 B per camera sample + 280 B per path vertex (the canonical f32 SoA wavefront's state traffic;
-    vertices = this run's device counter) over kernel_ms; peak 8.0 TB/s; frac = achieved / peak.
-    The megakernel does not stream that state (a path lives in registers), so this is the rate the
-    kernel's throughput corresponds to on §8(d)'s roofline, not bytes it moves. model_ceiling_Msamples
-    = 8 TB/s / (88 + 280 V) with V = vertices per sample: the rate at which that model reaches the HBM
-    peak (a faster kernel reads as beating the wavefront model, frac > 1, not as moving > 8 TB/s);
+HIP events recorded on the stream the kernel runs on). The megakernels keep every path in registers and
+read a scene of a few KB (cornell) from cache, so HBM does not bind them; f64 VALU issue does
+(the wait breakdown). The top-level fields therefore price the kernel against the FP64
+vector peak, every figure measured (roofline_block()):
+  * bound "fp64_valu": achieved = FP64 TFLOP/s of this run = the PMC-measured FP64 FLOP per path vertex
+    of this exact command (profiles/pmc_valu.json: (ADD_F64 + MUL_F64 + 2 FMA_F64) x 64 x lane
+    utilisation, tools/pmc_report.py) x this run's vertices (device counter) / kernel_ms; peak 78.6
+    TFLOP/s (MI355X FP64 vector); frac = achieved / peak, in [0, 1]. simd_valu_busy (SQ_ACTIVE_INST_VALU x
+    waves per SIMD, the SIMD's own VALU-busy share) stands beside it: an f64 path tracer also issues
+    integer, compare, select and 64-bit move VALU work, so the FP64 fraction alone understates how
+    full the VALU is;
   * traffic = the HBM bytes the PMC counters measured for one launch of this exact command
     (profiles/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE, separate rocprofv3 passes over
     `bench.py --steps 1 --warmup 0`, tools/gpu_task.sh benchpmc), scaled to this rank's rows; null
-    when no measurement exists for the workload. measured_frac = traffic / kernel_ms / peak;
+    when no measurement exists; hbm.frac = traffic / kernel_ms / 8 TB/s;
+  * wavefront_model: SURVEY §8(d)'s HBM model, 88 B per camera sample + 280 B per path vertex (the f32
+    SoA wavefront's state traffic) over kernel_ms; its frac can exceed 1 (a kernel that keeps paths in
+    registers beats the model), so it is a comparison, never the roofline fraction;
+    model_ceiling_Msamples = 8 TB/s / (88 + 280 V), V = vertices per sample;
   * minimum_bytes_per_launch = the megakernel's own unavoidable traffic: the f64 subpixel means
     written (4 x 3 x 8 B per pixel) and read back by the finalize, plus the RGB8 frame;
-  * binds = what limits the kernel: f64 VALU issue (the block "compute"): the PMC instruction mix per
-    path vertex of this command (profiles/pmc_valu.json, SQ passes of benchpmc, tools/pmc_report.py)
-    priced per class on a SIMD-32 (f64 add/mul/fma 4 cycles per wave64 instruction, f64
-    transcendental 8, 64-bit integer 4, other VALU 2) times this run's vertex rate, over 1024 SIMDs x
-    the PMC-measured clock; and the FP64 FLOP rate against 78.6 TFLOP/s.
+  * compute = the instruction-class issue model (f64 add/mul/fma 4 cycles per wave64 instruction,
+    f64 transcendental 8, 64-bit integer 4, other VALU 2) and the wait breakdown.
+Without a PMC mix for the workload (wavefront mode, f32, an unprofiled size) the line falls back to
+bound "hbm" with the measured traffic (or null), never the model.
 
 cpu_baseline: the CPU oracle (a line-by-line f64 restatement of the reference's sample loop; the
 reference itself is Rust and cannot be built here), compiled on this host with -O3 -march=native,
@@ -210,6 +215,48 @@ def compute_block(mix, vertices, kernel_ms):
     return out
 
 
+def roofline_block(mix, mix_source, vertices, samples, kernel_ms, traffic, traffic_source, kernel, min_bytes,
+                   binds):
+    """The bench line's roofline object (module docstring). mix: a profiles/pmc_valu.json entry of this
+    workload or None; vertices / samples: the launch's path vertices and camera samples; traffic: measured
+    HBM bytes per launch or None."""
+    sec = kernel_ms / 1e3
+    model_bytes = BYTES_PER_SAMPLE * samples + BYTES_PER_VERTEX * vertices
+    model_gbs = model_bytes / sec / 1e9
+    hbm_gbs = traffic / sec / 1e9 if traffic else None
+    out = {}
+    if mix and mix.get("fp64_flops_per_vertex"):
+        tflops = mix["fp64_flops_per_vertex"] * vertices / sec / 1e12
+        out.update({"bound": "fp64_valu", "achieved": round(tflops, 3), "peak": FP64_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(tflops / FP64_PEAK_TFLOPS, 4),
+                    "frac_meaning": "measured FP64 FLOP rate of the kernel over the MI355X FP64 vector peak",
+                    "fp64_flops_per_vertex": round(mix["fp64_flops_per_vertex"], 3),
+                    "flops_source": f"{mix.get('pmc_file') or mix_source}: {mix.get('source', '')}"})
+        if mix.get("waits"):
+            out["simd_valu_busy"] = round(mix["waits"]["simd_valu_busy"], 4)
+    else:
+        out.update({"bound": "hbm", "achieved": round(hbm_gbs, 2) if hbm_gbs is not None else None,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(hbm_gbs / HBM_PEAK_GBS, 6) if hbm_gbs is not None else None,
+                    "frac_meaning": "measured HBM bytes per launch over 8 TB/s (no PMC instruction mix for "
+                                    "this workload)"})
+    out.update({
+        "traffic": int(traffic) if traffic else None,
+        "traffic_source": traffic_source if traffic else None,
+        "hbm": {"achieved_GBps": round(hbm_gbs, 3) if hbm_gbs is not None else None, "peak_GBps": HBM_PEAK_GBS,
+                "frac": round(hbm_gbs / HBM_PEAK_GBS, 6) if hbm_gbs is not None else None},
+        "minimum_bytes_per_launch": min_bytes,
+        "wavefront_model_frac": round(model_gbs / HBM_PEAK_GBS, 4),
+        "wavefront_model": {"achieved_GBps": round(model_gbs, 2), "bytes_per_launch": model_bytes,
+                            "model": "SURVEY 8(d): 88 B per camera sample + 280 B per path vertex (f32 SoA "
+                                     "wavefront state), vertices from this run's device counter; a comparison "
+                                     "(> 1 means the kernel beats the streaming design), not bytes moved"},
+        "model_ceiling_Msamples": round(HBM_PEAK_GBS * 1e9 / (BYTES_PER_SAMPLE + BYTES_PER_VERTEX * vertices /
+                                                              samples) / 1e6, 1),
+        "kernel": kernel, "kernel_ms": round(kernel_ms, 3), "binds": binds})
+    return out
+
+
 def main():
     args = parse()
     import numpy as np
@@ -317,9 +364,6 @@ def main():
         # traffic was measured at N = 1 on the whole frame: scale to this rank's share of the rows
         traffic_full = load_profile("pmc_traffic.json", f"{workload} {mode}")
         traffic = int(traffic_full * th / args.height) if traffic_full else None
-        achieved = traffic / (dev_ms / 1e3) / 1e9 if traffic else None
-        model_bytes = BYTES_PER_SAMPLE * rank_samples + BYTES_PER_VERTEX * st["vertices"]
-        model_gbs = model_bytes / (dev_ms / 1e3) / 1e9
         npix = args.width * th
         alg_bytes = npix * (2 * 12 * 8 + 3)  # f64 subpixel means written + read by the finalize, RGB8 out
         out = {
@@ -348,31 +392,16 @@ def main():
                                      "meaningful)" if pinned not in (None, "") else "rank -> LOCAL_RANK",
                        "vertices": total_vertices,
                        "vertices_per_sample": round(total_vertices / n_samples, 4)},
-            "roofline": {"bound": "hbm",  # achieved / peak / frac below: the HBM model (binds: the real limit)
-                         "achieved": round(model_gbs, 2),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(model_gbs / HBM_PEAK_GBS, 4),
-                         "frac_meaning": "SURVEY 8(d)'s wavefront model: the f32 SoA state bytes this throughput "
-                                         "would stream, over 8 TB/s (a model ceiling, not bytes moved; the "
-                                         "megakernel keeps its paths in registers and is bound by f64 VALU issue, "
-                                         "roofline.compute)",
-                         "model_ceiling_Msamples": round(HBM_PEAK_GBS * 1e9 / (BYTES_PER_SAMPLE + BYTES_PER_VERTEX
-                                                         * st["vertices"] / rank_samples) / 1e6, 1),
-                         "traffic": traffic,
-                         "algorithmic_bytes_per_launch": model_bytes,
-                         "algorithmic_model": "SURVEY 8(d): 88 B per camera sample + 280 B per path vertex (f32 SoA "
-                                              "wavefront state), vertices from this run's device counter",
-                         "kernel": kernel, "kernel_ms": round(dev_ms, 3),
-                         "measured_frac": round(achieved / HBM_PEAK_GBS, 6) if achieved is not None else None,
-                         "traffic_source": "profiles/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE per launch, "
-                                           "rocprofv3 passes over this command)" if traffic else None,
-                         "minimum_bytes_per_launch": alg_bytes,
-                         "binds": "valu_issue_f64" if args.mode == "megakernel" else "launches_and_state_traffic"},
         }
-        # the instruction mix of this exact command (benchpmc), else of the scene's own PMC workload
-        mix = load_profile("pmc_valu.json", f"{workload} {mode}") or \
-            load_profile("pmc_valu.json", f"{args.scene} {mode}{' mis' if args.mis else ''}")
-        if mix and args.mode == "megakernel":
+        # the instruction mix of this exact command (benchpmc); only the exact workload prices the roofline
+        mix_key = f"{workload} {mode}"
+        mix = load_profile("pmc_valu.json", mix_key) if args.mode == "megakernel" else None
+        out["roofline"] = roofline_block(
+            mix, f"profiles/pmc_valu.json[{mix_key!r}]", st["vertices"], rank_samples, dev_ms, traffic,
+            "profiles/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE per launch, rocprofv3 passes over this "
+            "command)", kernel, alg_bytes,
+            "valu_issue_f64" if args.mode == "megakernel" else "launches_and_state_traffic")
+        if mix:
             out["roofline"]["compute"] = compute_block(mix, st["vertices"], dev_ms)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)

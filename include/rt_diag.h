@@ -36,6 +36,12 @@ int rt_debug_counters(unsigned long long out[16]);
  * (i < 16); RT_DEBUG_TIMERS builds: out[32 + i] = s_memtime ticks of the megakernel's waves in timed
  * region i (RT_DBG_TSTART / RT_DBG_TEND), summed over waves. */
 int rt_debug_regions(unsigned long long out[64]);
+/* The split tail (kernels/megakernel_common.h plan_tail) of the calling thread's last f64 megakernel
+ * render: out[0] = subpixels handed out as sample chunks (0: none split; only when spp / 4 >= 64),
+ * out[1] = how many the kernel family wanted before the scratch buffer capped it (out[0] < out[1]: the
+ * buffer was too small; the frame is the same, only the end of the launch balances worse), out[2] =
+ * samples per chunk. Returns 0. */
+int rt_debug_last_split(long long out[3]);
 #ifdef __cplusplus
 }
 #endif

@@ -36,6 +36,13 @@ struct RenderArgs {
     int32_t all_flat;              // every mesh is a flat octree (DevMesh::flat) and there are <= 2 of them
 };
 
+// The split tail the calling thread's last megakernel launch planned (plan_tail): subpixels split into
+// chunks, the split the kernel family wanted before the scratch buffer capped it, samples per chunk.
+// Thread-local: a render is planned and enqueued on its caller's thread (rt_debug_last_split, rt_diag.h).
+struct TailPlan {
+    long n_split = 0, want = 0, chunk = 0;
+};
+extern thread_local TailPlan t_tail_plan;
 // Split-tail scratch bytes per split subpixel (megakernel_common.h plan_tail: the samples after chunk 0).
 size_t tail_scratch_per_subpixel(int n_samples);
 // tail_buf / tail_cap: scratch for the split tail (bytes); the launcher sizes the tail to fit it.

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "../ab_knobs.h"
 #include "kernels.h"
 
 namespace rt {
@@ -224,10 +225,8 @@ static inline long resident_blocks(K kernel, long want, int threads = 256) {
     return std::max(1L, std::min((long)ncu * per_cu, want));
 }
 
-static inline int env_int(const char* name, int dflt) {
-    const char* v = std::getenv(name);
-    return v ? std::atoi(v) : dflt;
-}
+// A/B overrides (ab_knobs.h): RT_* environment variables in -DRT_AB_KNOBS=1 builds only
+static inline int env_int(const char* name, int dflt) { return (int)ab_knob(name, dflt); }
 
 #ifndef RT_MK_W4
 #define RT_MK_W4 4  // waves/SIMD of the analytic-scene kernel (A/B builds: -DRT_MK_W4=5)
@@ -279,9 +278,12 @@ static inline void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_
     a.tail_cps = (a.n_samples + (1 << a.chunk_lg) - 1) >> a.chunk_lg;
     // chunk 0 of a split subpixel sums in place (tail_stores): scratch only for the samples after it
     const size_t per_sub = (size_t)std::max(0, a.n_samples - (1 << a.chunk_lg)) * 3 * sizeof(double);
-    long n_split = 0;
-    if (tail_env && tail_buf && a.n_samples >= 64 && a.tail_cps >= 2 && per_sub > 0)
-        n_split = std::min({split_want, nsub / std::max(1, cap_div), (long)(tail_cap / per_sub)});
+    long n_split = 0, want = 0;
+    if (tail_env && a.n_samples >= 64 && a.tail_cps >= 2 && per_sub > 0) {
+        want = std::min(split_want, nsub / std::max(1, cap_div));
+        if (tail_buf) n_split = std::min(want, (long)(tail_cap / per_sub));
+    }
+    if (nsub > 0) t_tail_plan = TailPlan{n_split, want, 1L << a.chunk_lg};  // rt_debug_last_split
     a.n_whole = (int32_t)(nsub - n_split);
     a.tail_buf = tail_buf;
     plan_units(a, lanes);

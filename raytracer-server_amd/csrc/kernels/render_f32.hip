@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 #include "../device/integrator_f64.h"  // Rng, subpixel_of (integer work shared with the f64 path)
+#include "../ab_knobs.h"
 #include "kernels.h"
 
 #ifndef RT_F32_W
@@ -685,7 +686,7 @@ static hipError_t launch_w(const DevScene& sc, const RenderArgs& a, double* sub_
 template <bool MESH, bool MIS>
 static hipError_t launch_k(const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
                            hipStream_t st) {
-    static const int env = [] { const char* v = std::getenv("RT_F32_WAVES"); return v ? std::atoi(v) : 0; }();
+    static const int env = (int)ab_knob("RT_F32_WAVES", 0);
     // deep meshes (the unicorn's BVH walks) hide their node-load latency with more waves:
     // 8 waves/SIMD +12% there, cubes and cornell -20% (profiles/r01h_fp32.log)
     const int w = env ? env : (MESH && a.mesh_nodes >= 64 ? RT_F32_W_MESH : RT_F32_W);

@@ -256,6 +256,8 @@ __global__ __launch_bounds__(256) void k_trace_f64(DevScene sc, long n, const do
     }
 }
 
+thread_local TailPlan t_tail_plan;
+
 template <int F, int W>
 static void launch_mk(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub, long nsub,
                       int refill, double* tail_buf, size_t tail_cap, hipStream_t st) {
@@ -271,6 +273,23 @@ static void launch_mk(const DevScene& sc, const RenderArgs& a_in, double* sub_bu
     }
 }
 
+// The analytic / fused-mesh megakernel at its waves/SIMD: 4 for analytic scenes, 3 with meshes (the defaults);
+// A/B builds (ab_knobs.h) compile both shapes of every instance for RT_MK_WAVES.
+template <int F>
+static void launch_mk_shape(int waves, const DevScene& sc, const RenderArgs& a, double* sub_buf, uint32_t* next_sub,
+                            long nsub, int refill, double* tail_buf, size_t tail_cap, hipStream_t st) {
+    if constexpr (RT_AB_KNOBS != 0) {
+        if (waves == 3) launch_mk<F, 3>(sc, a, sub_buf, next_sub, nsub, refill, tail_buf, tail_cap, st);
+        else launch_mk<F, RT_MK_W4>(sc, a, sub_buf, next_sub, nsub, refill, tail_buf, tail_cap, st);
+    } else if constexpr ((F & 1) != 0) {
+        (void)waves;
+        launch_mk<F, 3>(sc, a, sub_buf, next_sub, nsub, refill, tail_buf, tail_cap, st);
+    } else {
+        (void)waves;
+        launch_mk<F, RT_MK_W4>(sc, a, sub_buf, next_sub, nsub, refill, tail_buf, tail_cap, st);
+    }
+}
+
 hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, double* sub_buf, uint32_t* next_sub,
                                  double* tail_buf, size_t tail_cap, hipStream_t st) {
     RenderArgs a = a_in;
@@ -279,6 +298,7 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, dou
     a.tail_cps = 1;
     const long nsub = (long)a.tw * a.th * 4;
     if (nsub <= 0 || a.n_samples <= 0) return hipSuccess;
+    t_tail_plan = TailPlan{};
     hipError_t e = hipMemsetAsync(next_sub, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     // Occupancy (waves/SIMD requested from the register allocator): 4 (128 VGPRs, a few spills)
@@ -319,8 +339,7 @@ hipError_t launch_megakernel_f64(const DevScene& sc, const RenderArgs& a_in, dou
     }
 #define RT_MK_CASE(F)                                                           \
     case F:                                                                     \
-        if (waves == 3) launch_mk<F, 3>(sc, a, sub_buf, next_sub, nsub, refill, tail_buf, tail_cap, st);  \
-        else launch_mk<F, RT_MK_W4>(sc, a, sub_buf, next_sub, nsub, refill, tail_buf, tail_cap, st);      \
+        launch_mk_shape<F>(waves, sc, a, sub_buf, next_sub, nsub, refill, tail_buf, tail_cap, st); \
         break;
     switch (a.features & 15) {
         RT_MK_CASE(0) RT_MK_CASE(1) RT_MK_CASE(2) RT_MK_CASE(3) RT_MK_CASE(4) RT_MK_CASE(5) RT_MK_CASE(6)
@@ -388,6 +407,15 @@ __global__ void k_selftest_arith(long n, uint64_t seed, unsigned long long* bad)
     if (e & 1) atomicAdd(&bad[0], 1ull);
     if (e & 2) atomicAdd(&bad[1], 1ull);
     if (e & 4) atomicAdd(&bad[2], 1ull);
+}
+
+// The split tail of the calling thread's last megakernel launch (kernels.h TailPlan).
+extern "C" int rt_debug_last_split(long long out[3]) {
+    if (!out) return -1;
+    out[0] = t_tail_plan.n_split;
+    out[1] = t_tail_plan.want;
+    out[2] = t_tail_plan.chunk;
+    return 0;
 }
 
 // n_out: the caller's output count (at most 3 are written: reciprocal, quotient, square root)

@@ -888,6 +888,9 @@ hipError_t launch_megakernel_flat_f64(const DevScene& sc, const RenderArgs& a_in
     // kernel's `refill` is 40)
     static const int fpool_refill = env_int("RT_MK_FPOOL_REFILL", 20);
     (void)refill;
+    // Product builds: the query pool at 3 waves/SIMD. The block-synchronous flat kernel (RT_MK_FPOOL=0) and the
+    // 2-wave shapes exist only in A/B builds (ab_knobs.h).
+#if RT_AB_KNOBS
 #define RT_FLAT_CASE(F)                                                                       \
     case F:                                                                                   \
         if (fpool) {                                                                          \
@@ -896,6 +899,13 @@ hipError_t launch_megakernel_flat_f64(const DevScene& sc, const RenderArgs& a_in
         } else if (waves == 2) launch_flat<F, 2>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, st); \
         else launch_flat<F, 3>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, st); \
         break;
+#else
+#define RT_FLAT_CASE(F)                                                                       \
+    case F:                                                                                   \
+        (void)waves;                                                                          \
+        launch_fpool<F, 3>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); \
+        break;
+#endif
     if (fpool && nospec && (a.features & 32) && !(a.features & 2)) {  // no mirror, no Phong object
         switch (a.features & 15) {
             case 9: launch_fpool<9 | 32, RT_FPOOL_BLOCK / 256, RT_FPOOL_BLOCK>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, pool_min, fpool_refill, st); break;

@@ -1276,17 +1276,26 @@ hipError_t launch_megakernel_mesh_f64(const DevScene& sc, const RenderArgs& a, d
     static const int ksteps = std::max(1, env_int("RT_MK_KSTEPS", 4));
     // 2: the role-split pool (k_megakernel_roles_f64: unicorn 1920x1080x512 269.9 -> 310.6 Msamples/s,
     // profiles/r05c_ab_c4.log); 1: the round-4 walk pool (every wave walks and shades its own paths); 0: per-lane walks
-    static const int pool = env_int("RT_MK_POOL", 2);
+    [[maybe_unused]] static const int pool = env_int("RT_MK_POOL", 2);
     static const int pool_min = env_int("RT_MK_POOL_MIN", 48);  // 48 with the 512-thread pool (32 before)
     static const int pool_ksteps = std::max(1, env_int("RT_MK_POOL_KSTEPS", 6));
     static const int pool_vmin = env_int("RT_MK_POOL_VMIN", 0);
     static const int pool_refill = env_int("RT_MK_POOL_CAM_REFILL", 20);  // the walk pool's camera refill threshold
+    // Product builds: the role-split pool, or the walk pool over node_kids for an octree without slot tables. The
+    // superseded slot-walk instances (the round-4 walk pool, RT_MK_POOL=1; per-lane walks, RT_MK_POOL=0) exist
+    // only in A/B builds (ab_knobs.h).
+#if RT_AB_KNOBS
+#define RT_MM_AB(F)                                                                            \
+        else if (pool == 1) launch_mm<F, 2, 1>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, pool_refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
+        else if (pool == 0) launch_mm<F, 2, 0>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, 0, 0, tail_buf, tail_cap, st);
+#else
+#define RT_MM_AB(F)
+#endif
 #define RT_MM_CASE(F)                                                                          \
     case F:                                                                                    \
         if (!sc.node_slot) launch_mm<F, 2, 1, false>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, pool_refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
-        else if (pool == 2) launch_roles<F>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, st); \
-        else if (pool) launch_mm<F, 2, 1>(sc, a, sub_buf, next_sub, nsub, pool_ksteps, wmin, pool_refill, pool_min, pool_vmin, tail_buf, tail_cap, st); \
-        else launch_mm<F, 2, 0>(sc, a, sub_buf, next_sub, nsub, ksteps, wmin, refill, 0, 0, tail_buf, tail_cap, st); \
+        RT_MM_AB(F)                                                                            \
+        else launch_roles<F>(sc, a, sub_buf, next_sub, nsub, tail_buf, tail_cap, st);          \
         break;
 #define RT_MMB_CASE(F)                                                                         \
     case F:                                                                                    \
@@ -1299,6 +1308,7 @@ hipError_t launch_megakernel_mesh_f64(const DevScene& sc, const RenderArgs& a, d
     }
 #undef RT_MMB_CASE
 #undef RT_MM_CASE
+#undef RT_MM_AB
     return hipGetLastError();
 }
 

@@ -25,6 +25,7 @@
 
 #include "../device/integrator_f64.h"
 #include "wavefront.h"
+#include "../ab_knobs.h"
 
 namespace rt {
 using namespace f64;
@@ -396,10 +397,9 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(DevScene sc, RenderArgs a, 
     }
 }
 
+// A/B overrides of the stream shape (ab_knobs.h: -DRT_AB_KNOBS=1 builds only)
 size_t env_size(const char* name, size_t dflt) {
-    const char* v = std::getenv(name);
-    if (!v || !*v) return dflt;
-    long long x = std::atoll(v);
+    const long x = ab_knob(name, (long)dflt);
     return x > 0 ? (size_t)x : dflt;
 }
 

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/rt_ffi.h"
+#include "ab_knobs.h"
 #include "device/scene_layout.h"
 #include "host/scene_host.hpp"
 #include "kernels/kernels.h"
@@ -126,10 +127,7 @@ void cp3(double* dst, const rt::host::D3& v) {
 // RT_BVH_SAH=0 selects the median-split build (A/B); default: binned SAH.
 constexpr int kBins = 16;      // SAH bins per axis
 constexpr int kSahDepth = 16;  // deeper BVH nodes split at the median (depth stays <= kBvhMaxDepth)
-bool bvh_sah_enabled() {
-    const char* v = std::getenv("RT_BVH_SAH");
-    return !(v && std::atoi(v) == 0);
-}
+bool bvh_sah_enabled() { return rt::ab_knob("RT_BVH_SAH", 1) != 0; }
 
 void build_bvh(Packed& p, const rt::host::Mesh& m, int32_t tri_base) {
     using rt::host::D3;
@@ -1079,7 +1077,7 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
                 if (ws->ensure_tail(want) != hipSuccess) (void)hipGetLastError();  // no tail split then
             }
             if (fp32) {
-                static const int brute = [] { const char* v = std::getenv("RT_F32_BRUTE"); return v ? std::atoi(v) : 16; }();
+                static const int brute = (int)rt::ab_knob("RT_F32_BRUTE", 16);
                 a.f32_brute = brute;
                 e = rt::launch_megakernel_f32(ds, a, sub, (uint32_t*)(ws->counters + 4), st);
             } else {

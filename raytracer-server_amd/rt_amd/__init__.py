@@ -118,6 +118,8 @@ def _load():
         L.rt_debug_counters.argtypes = [P(ctypes.c_ulonglong)]
     if hasattr(L, "rt_debug_regions"):
         L.rt_debug_regions.argtypes = [P(ctypes.c_ulonglong)]
+    if hasattr(L, "rt_debug_last_split"):
+        L.rt_debug_last_split.argtypes = [P(ctypes.c_longlong)]
     return L
 
 
@@ -378,6 +380,15 @@ def debug_qcheck():
     if rc < 0:
         raise RtError(rc, "rt_debug_qcheck")
     return None if rc == 1 else [int(v) for v in out]
+
+
+def debug_last_split():
+    """The split tail of this thread's last f64 megakernel render (rt_diag.h rt_debug_last_split):
+    dict(split=subpixels handed out as sample chunks, want=the kernel family's split before the scratch
+    buffer capped it, chunk=samples per chunk)."""
+    out = (ctypes.c_longlong * 3)()
+    _check(lib.rt_debug_last_split(out))
+    return dict(split=int(out[0]), want=int(out[1]), chunk=int(out[2]))
 
 
 def device_count():

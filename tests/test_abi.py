@@ -27,7 +27,7 @@ def test_exports_diagnostics(rt):
     text = open(os.path.join(REPO, "include", "rt_diag.h")).read()
     names = re.findall(r"^int\s+(rt_[a-z_0-9]+)\s*\(", text, re.M)
     assert names == ["rt_selftest_arith_n", "rt_selftest_arith", "rt_selftest_tables", "rt_debug_qcheck",
-                     "rt_debug_counters", "rt_debug_regions"]
+                     "rt_debug_counters", "rt_debug_regions", "rt_debug_last_split"]
     for n in names:
         assert hasattr(rt.lib, n), f"missing export {n}"
     assert rt.debug_qcheck() is None  # the product library is built without the protocol checks
@@ -103,3 +103,18 @@ def test_band_plan_covers_tile_in_order(rt):
                 else:
                     assert len(rows) <= 8 * workers and (th < 8 * workers or len(rows) >= 4 * workers)
     assert rt.band_plan(0, 4, 0) == ([], [])
+
+
+def test_product_library_reads_no_tuning_switches(rt):
+    """The RT_* A/B switches (ab_knobs.h) are compiled into the A/B build only: the product library holds
+    none of their names, so no environment variable can select another kernel or shape in a server
+    process. Only the two RT_TEST_* hooks remain (they force the exact fallback tables of oversized
+    octrees, for tests)."""
+    blob = open(rt.LIB_PATH, "rb").read()
+    names = set(re.findall(rb"RT_[A-Z0-9_]{3,}", blob))
+    switches = {n for n in names if not n.startswith((b"RT_FLAG_", b"RT_TEST_", b"RT_E_", b"RT_OK"))}
+    assert not switches, sorted(switches)
+    assert not re.search(rb"RT_MK_", blob)
+    ab = os.path.join(REPO, "raytracer-server_amd", "lib", "variants", "ab.so")
+    if os.path.exists(ab):  # the A/B build does read them
+        assert b"RT_MK_POOL" in open(ab, "rb").read()

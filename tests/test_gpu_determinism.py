@@ -111,16 +111,20 @@ print(json.dumps(out))
 @pytest.mark.parametrize("env", [{"RT_MK_FPOOL": "0"}, {"RT_MK_POOL": "0"}, {"RT_MK_NOSPEC": "0"},
                                  {"RT_MK_FPOOL_REFILL": "0", "RT_MK_POOL_CAM_REFILL": "0"}])
 def test_kernel_variants_render_the_default_frames(env):
-    """The A/B kernel variants behind RT_* switches (read once per process, so each in a subprocess):
-    the block-synchronous flat kernel (RT_MK_FPOOL=0), per-lane octree walks (RT_MK_POOL=0), the
-    mirror-capable query-pool instance on the mirror-free
-    cubes (RT_MK_NOSPEC=0: the default runs Cfg bit 32) and both pools without their camera-sample
-    refill pass render byte-identical frames to the defaults."""
+    """The A/B kernel variants behind RT_* switches, which only the A/B build reads (ab_knobs.h:
+    lib/variants/ab.so, -DRT_AB_KNOBS=1; read once per process, so each in a subprocess): the
+    block-synchronous flat kernel (RT_MK_FPOOL=0), per-lane octree walks (RT_MK_POOL=0), the
+    mirror-capable query-pool instance on the mirror-free cubes (RT_MK_NOSPEC=0: the default runs Cfg
+    bit 32) and both pools without their camera-sample refill pass render byte-identical frames to the
+    product library's defaults; the product library under the same switches renders them too (it
+    reads none of them)."""
+    ab = os.path.join(REPO, "raytracer-server_amd", "lib", "variants", "ab.so")
+    assert os.path.exists(ab), f"{ab} not built (make -C raytracer-server_amd ab)"
     base = dict(os.environ, RT_REPO=REPO)
-    for k in ("RT_MK_FPOOL", "RT_MK_POOL", "RT_MK_NOSPEC", "RT_MK_FPOOL_REFILL", "RT_MK_POOL_CAM_REFILL"):
+    for k in ("RT_MK_FPOOL", "RT_MK_POOL", "RT_MK_NOSPEC", "RT_MK_FPOOL_REFILL", "RT_MK_POOL_CAM_REFILL", "RT_AMD_LIB"):
         base.pop(k, None)
     runs = []
-    for e in ({}, env):
+    for e in ({}, dict(env, RT_AMD_LIB=ab), env):
         out = subprocess.run([sys.executable, "-c", _VARIANT_SCRIPT], env=dict(base, **e), capture_output=True,
                              text=True, timeout=240)
         assert out.returncode == 0, out.stderr[-3000:]

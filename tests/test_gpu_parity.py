@@ -142,6 +142,43 @@ def test_split_tail_equals_wavefront(rt, gpu_scenes):
             assert a[2]["vertices"] == b[2]["vertices"]
 
 
+@pytest.mark.parametrize("name,mis", [("cornell_box", False), ("cubes", False), ("flying_unicorn", False),
+                                      ("chair_phong", True)])
+def test_split_tail_parity_against_oracle(name, mis, rt, gpu_scenes, oracle_scenes, oracle, tmp_path):
+    """The split tail of every megakernel family against the oracle (1e-9 / RGB8), at 256 spp (64 samples per
+    subpixel: the smallest spp that splits, plan_tail): chunk 0 of a split subpixel sums in place in sub_buf,
+    the later chunks store each sample's radiance at tail_slot, and k_tail_sum_f64 continues chunk 0's partial
+    sum. cornell: the analytic kernel (half the frame split); cubes: the 1024-thread query pool; the unicorn:
+    the role-split pool (the whole frame split, six subpixels per path slot); a Phong chair with MIS: the
+    512-thread Phong / MIS role-pool instance. The launch must have split subpixels (rt_debug_last_split)."""
+    if name == "chair_phong":
+        from test_host_prep import extra_asset_scene
+
+        p = extra_asset_scene(tmp_path, "chair.obj")
+        text = open(p).read()
+        floor = '{ type = "diffuse", kd = [0.75, 0.75, 0.75] }\ngeometry = { type = "plane", pos = [0.0, 0.0, 0.0]'
+        assert floor in text
+        text = text.replace(floor, floor.replace('{ type = "diffuse", kd = [0.75, 0.75, 0.75] }',
+                                                 '{ type = "phong", kd = 0.5, ks = 0.3, power = 8, color_d = [0.7, 0.6, '
+                                                 '0.5], color_s = [1.0, 1.0, 1.0] }'))
+        open(p, "w").write(text)
+        sc, orc = rt.Scene.from_toml(p), oracle.OracleScene(p)
+    else:
+        sc, orc = gpu_scenes[name], oracle_scenes[name]
+    w, h, spp = 32, 24, 256
+    tile = (0, 0, w, h) if name != "flying_unicorn" else None
+    if name == "flying_unicorn":  # the mesh's part of the frame (a 32x24 crop of 640x480)
+        w, h, tile = 640, 480, (300, 230, 32, 24)
+    rgb_g, sub_g, st = rt.render(sc, w, h, spp, SEED, tile=tile, mis=mis, megakernel=True, want_sub=True)
+    plan = rt.debug_last_split()
+    nsub = tile[2] * tile[3] * 4
+    assert plan["chunk"] == 32 and 0 < plan["split"] <= nsub, plan
+    if name in ("flying_unicorn", "chair_phong"):
+        assert plan["split"] == nsub, plan  # the walk kernels split the whole frame when it is this small
+    rgb_o, sub_o, st_o = orc.render(w, h, spp, SEED, tile=tile, mis=mis)
+    _assert_parity(rgb_g, sub_g, rgb_o, sub_o, f"{name}/split tail")
+
+
 def test_tiling_invariance_and_determinism(rt, gpu_scenes):
     s = gpu_scenes["cubes"]
     w, h = 200, 150

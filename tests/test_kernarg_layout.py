@@ -16,15 +16,18 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 LIB = os.path.join(REPO, "raytracer-server_amd", "lib", "librtamd.so")
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 # kernels whose bodies call karg_scene() / karg_render_args() (RT_KARG_VIEW), by mangled-name stem
-VIEW_KERNELS = ("k_megakernel_f64", "k_megakernel_mesh_f64", "k_megakernel_fpool_f64", "k_megakernel_flat_f64",
+VIEW_KERNELS = ("k_megakernel_f64", "k_megakernel_mesh_f64", "k_megakernel_roles_f64", "k_megakernel_fpool_f64",
                 "k_selftest_tables")
+# superseded kernels compiled only into the A/B build (ab_knobs.h: lib/variants/ab.so)
+AB_VIEW_KERNELS = ("k_megakernel_flat_f64",)
+AB_LIB = os.path.join(REPO, "raytracer-server_amd", "lib", "variants", "ab.so")
 
 
-def _kernels(tmp_path):
+def _kernels(tmp_path, lib=LIB):
     if not os.path.exists(os.path.join(LLVM, "clang-offload-bundler")):
         pytest.skip("ROCm LLVM tools not installed")
     fb = tmp_path / "fatbin.bin"
-    subprocess.run([f"{LLVM}/llvm-objcopy", "-O", "binary", "--only-section=.hip_fatbin", LIB, str(fb)], check=True)
+    subprocess.run([f"{LLVM}/llvm-objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib, str(fb)], check=True)
     data = fb.read_bytes()
     starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
     assert starts, "no offload bundle in librtamd.so"
@@ -47,13 +50,19 @@ def _kernels(tmp_path):
     return out
 
 
-def test_kernarg_views_match_every_megakernel_signature(tmp_path):
-    ks = _kernels(tmp_path)
+@pytest.mark.parametrize("which", ["product", "ab"])
+def test_kernarg_views_match_every_megakernel_signature(which, tmp_path):
+    if which == "ab" and not os.path.exists(AB_LIB):
+        pytest.skip("lib/variants/ab.so not built (make -C raytracer-server_amd ab)")
+    ks = _kernels(tmp_path, LIB if which == "product" else AB_LIB)
+    stems = VIEW_KERNELS + (AB_VIEW_KERNELS if which == "ab" else ())
     hits = {k: v for k, v in ks.items() if any(re.search(rf"\d{stem}I", k) or re.search(rf"\d{stem}E", k)
-                                                for stem in VIEW_KERNELS)}
-    # every megakernel family is present (the product library instantiates each)
-    for stem in VIEW_KERNELS:
-        assert any(stem in k for k in hits), f"no {stem} instance in the code objects"
+                                                for stem in stems)}
+    # every megakernel family is present (the library instantiates each), the role-split pool included
+    for stem in stems:
+        assert any(re.search(rf"\d{stem}[IE]", k) for k in hits), f"no {stem} instance in the code objects"
+    if which == "product":  # the superseded kernels are gone from the product library
+        assert not any(stem in k for k in ks for stem in AB_VIEW_KERNELS)
     for name, args in hits.items():
         assert "NS_8DevSceneENS_10RenderArgsE" in name, f"{name}: (DevScene, RenderArgs) are not the first two parameters"
         assert args[0] == (0, 248), f"{name}: DevScene at {args[0]} (karg_scene reads offset 0, 248 bytes)"

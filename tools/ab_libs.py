@@ -1,7 +1,8 @@
 """A/B of library builds on one GPU: python tools/ab_libs.py SCENE W H SPP LIB[,LIB...] [ROUNDS] [extra prof_render args]
 
 Each LIB (a path to a librtamd.so build, e.g. lib/variants/base.so; "main" = lib/librtamd.so; an
-optional "@VAR=VAL[+VAR=VAL]" suffix sets RT_* switches for that entry, e.g. main@RT_MK_POOL=2) renders
+optional "@VAR=VAL[+VAR=VAL]" suffix sets RT_* switches for that entry, e.g.
+raytracer-server_amd/lib/variants/ab.so@RT_MK_POOL=1 — only the A/B build reads them, ab_knobs.h) renders
 the same frame in its own process (tools/prof_render.py under RT_AMD_LIB), ROUNDS times in alternating
 order, so clock drift hits every build alike. Prints device time, Msamples/s and the frame's sha1 per
 run (identical digests = identical frames), then the median per build."""

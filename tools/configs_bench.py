@@ -125,7 +125,6 @@ for label, name, w, h, spp, mis in CONFIGS:
         print(json.dumps({"config": label, "value": 0.0, "unit": "Msamples/s", "note": "spp/4 = 0: no samples"}), flush=True)
         continue
     sec = st["device_ms"] / 1e3
-    model = bench.BYTES_PER_SAMPLE * n + bench.BYTES_PER_VERTEX * st["vertices"]
     line = {"metric": f"Msamples/sec {name} {w}x{h}x{spp}spp{' mis' if mis else ''}", "config_label": label,
             "value": round(rate, 3), "unit": "Msamples/s", "n_gpus": 1, "higher_is_better": True,
             "dtype": "f32" if fp32 else "f64", "data": "synthetic: reference scene file + counter-based RNG, seed 0x5eed",
@@ -133,14 +132,15 @@ for label, name, w, h, spp, mis in CONFIGS:
                        "spp": spp, "mis": mis, "mode": "megakernel" + ("-f32" if fp32 else ""),
                        "vertices": st["vertices"], "vertices_per_sample": round(st["vertices"] / n, 4),
                        "device_ms": round(st["device_ms"], 3)},
-            "roofline": {"bound": "valu_issue_f64" if not fp32 else "valu_issue_f32",
-                         "achieved": round(model / sec / 1e9, 2), "peak": bench.HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(model / sec / 1e9 / bench.HBM_PEAK_GBS, 4),
-                         "frac_meaning": "SURVEY 8(d)'s wavefront model (a model ceiling, not bytes moved)",
-                         "model_ceiling_Msamples": round(bench.HBM_PEAK_GBS * 1e9 / (bench.BYTES_PER_SAMPLE +
-                                                         bench.BYTES_PER_VERTEX * st["vertices"] / n) / 1e6, 1),
-                         "traffic": None, "algorithmic_bytes_per_launch": model,
-                         "algorithmic_model": "SURVEY 8(d): 88 B per camera sample + 280 B per path vertex"}}
+            }
+    pmc, src, exact = pmc_summary(name, w, h, spp, mis) if not fp32 else (None, None, False)
+    # only a PMC summary of exactly this workload prices the roofline (FP64 FLOP per vertex, measured traffic)
+    mix = dict(pmc["valu_mix"], waits=pmc.get("waits"), source=pmc.get("kernel") or "") if (pmc and exact) else None
+    hbm = pmc.get("hbm") if (pmc and exact) else None
+    line["roofline"] = bench.roofline_block(
+        mix, src, st["vertices"], n, st["device_ms"], hbm["bytes"] if hbm else None,
+        f"{src}: 2 x FETCH_SIZE + WRITE_SIZE of this workload's launch", "k_megakernel", None,
+        "valu_issue_f64" if not fp32 else "valu_issue_f32")
     if name != "cornell_box" and not fp32:
         wc = walk_counters(name, w, h, mis, spp)
         if wc and wc["vertices"] and wc["calls"] and not (wc["parent_visits"] or wc["leaves"] or wc["tri_tests"]):
@@ -159,26 +159,16 @@ for label, name, w, h, spp, mis in CONFIGS:
                 "walks_per_vertex": round(per_v["calls"], 4),
                 "per_walk": {k: round(wc[k] / max(1, wc["calls"]), 3) for k in ("parent_visits", "leaves", "tri_tests")},
                 "source": "walk counters of lib/variants/dbg.so (RT_DEBUG_COUNTERS) on this workload"}
-    pmc, src, exact = pmc_summary(name, w, h, spp, mis) if not fp32 else (None, None, False)
     if pmc:
         rf = line["roofline"]
         rf["compute"] = bench.compute_block(pmc["valu_mix"], st["vertices"], st["device_ms"])
-        rf["compute"]["source"] = src
+        rf["compute"]["source"] = src if exact else f"{src} (another size of this scene: per-vertex mix only)"
         rf["compute"]["kernel"] = pmc.get("kernel")
         if pmc.get("waits"):
             rf["compute"]["simd_valu_busy"] = round(pmc["waits"]["simd_valu_busy"], 4)
             rf["compute"]["wait_any"] = round(pmc["waits"]["wait_any"], 4)
-        hbm = pmc.get("hbm")
-        if hbm and pmc.get("samples"):
-            # the measured HBM bytes of the launch (2 x FETCH_SIZE + WRITE_SIZE); from another size of the same
-            # scene scaled per sample (labelled)
-            traffic = hbm["bytes"] if exact else hbm["bytes"] / pmc["samples"] * n
-            rf["traffic"] = int(traffic)
-            rf["measured_frac"] = round(traffic / sec / 1e9 / bench.HBM_PEAK_GBS, 6)
-            rf["traffic_source"] = (f"{src}: 2 x FETCH_SIZE + WRITE_SIZE of this workload's launch" if exact else
-                                    f"{src}: 2 x FETCH_SIZE + WRITE_SIZE per sample of {pmc['workload']}, x {n} samples")
-            if pmc.get("l2_hit_rate") is not None:
-                rf["l2_hit_rate"] = round(pmc["l2_hit_rate"], 4)
+        if exact and pmc.get("l2_hit_rate") is not None:
+            rf["l2_hit_rate"] = round(pmc["l2_hit_rate"], 4)
     c = cpu.get(label.split(" (")[0]) or next((v for k, v in cpu.items() if k.startswith(label.split(" (")[0])), None)
     if c:
         line["cpu_baseline"] = {"value": c["all_cores"]["Msamples_per_s"], "unit": "Msamples/s", "cores": c["cores"],

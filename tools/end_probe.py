@@ -1,6 +1,7 @@
 """Where a rank share's fixed ~10 ms goes: device time of the analytic megakernel on tiles of the
 cornell frame, contiguous (row_step 1) and interleaved (row_step N), against the full frame's
-per-sample rate. python tools/end_probe.py [spp] [scene]"""
+per-sample rate. python tools/end_probe.py [spp] [scene]
+RT_MK_TAIL / RT_MK_TAIL_CPS act only in the A/B build: run it with RT_AMD_LIB=.../lib/variants/ab.so."""
 import os
 import sys
 

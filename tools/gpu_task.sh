@@ -123,7 +123,7 @@ for task in "$@"; do
     dbgbuild)
         # diagnostic library (RT_DEBUG_COUNTERS + RT_DEBUG_TIMERS) at raytracer-server_amd/lib/variants/dbg.so
         make -s -j16 -C raytracer-server_amd BUILD=build_dbg LIB=lib/variants/dbg.so \
-            EXTRA="-DRT_DEBUG_COUNTERS=1 -DRT_DEBUG_TIMERS=1" > "$OUT/dbgbuild.log" 2>&1 || fail dbgbuild "$OUT/dbgbuild.log"
+            EXTRA="-DRT_DEBUG_COUNTERS=1 -DRT_DEBUG_TIMERS=1 -DRT_AB_KNOBS=1" > "$OUT/dbgbuild.log" 2>&1 || fail dbgbuild "$OUT/dbgbuild.log"
         echo "dbg build ok" ;;
     env)
         # env:VAR=VAL[,VAR=VAL...] applies to the tasks after it (A/B runs of the RT_* switches)

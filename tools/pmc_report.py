@@ -2,7 +2,8 @@
 
 usage: python tools/pmc_report.py gpurun_out/<TAG> <key> [kernel-substring] [--out profiles/<file>.json]
                                   [--valu-key "<scene> <mode>" --valu-out profiles/pmc_valu.json]
-(--valu-key merges the per-vertex instruction mix into the map bench.py's roofline.compute reads)
+(--pmc-file profiles/<name>.json records, in that map entry, the committed summary the mix comes from;
+--valu-key merges the per-vertex instruction mix into the map bench.py's roofline.compute reads)
 
 Per MI355X_MICROARCH.md:
   * HBM bytes = 2 x FETCH_SIZE (gfx950 counts half the bytes of wide reads) + WRITE_SIZE, both KiB;
@@ -142,6 +143,8 @@ def main():
             os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_valu.json")
         m = json.load(open(path)) if os.path.exists(path) else {}
         m[vk] = r["valu_mix"]
+        if "--pmc-file" in sys.argv:  # the committed summary this mix came from (bench.py's roofline names it)
+            m[vk]["pmc_file"] = sys.argv[sys.argv.index("--pmc-file") + 1]
         json.dump(m, open(path, "w"), indent=1)
 
 
