@@ -707,6 +707,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
                 nverts += h.obj >= 0;
                 ShadowDefer df;
                 df.pending = false;
+                df.c = v3(0.0, 0.0, 0.0);
 #if RT_FPOOL_SINK
                 // the shadow query's ray goes straight into this lane's query columns (its s_pend read 0)
                 const LdsQuerySink qsink{(LdsD*)s_qo + tid, (LdsD*)s_qds + tid, B};
@@ -715,9 +716,13 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
                 const bool cont = shade_vertex<C, Cold>(sc, a, ps, h, &df, cold);
 #endif
                 traced = false;
+                // pc is read only after a shadow query set it (spend): taking df.c unconditionally makes the old
+                // value dead through shade_vertex, the kernel's register peak (the 1024-thread instance: 29 -> 21
+                // spilled VGPRs, 76 -> 48 B of scratch per lane; cubes 1920x1080x256 1042.1 -> 1067.1 Msamples/s,
+                // profiles/r06b_ab_pcdead.log)
+                pc = df.c;
                 if (df.pending) {  // the analytic objects let the shadow ray through; a mesh may block it
                     shadow_q = true;
-                    pc = df.c;
 #if !RT_FPOOL_SINK
                     dist = df.dist;
                     sr = Ray{df.o, df.d};
