@@ -42,6 +42,13 @@ int rt_debug_regions(unsigned long long out[64]);
  * buffer was too small; the frame is the same, only the end of the launch balances worse), out[2] =
  * samples per chunk. Returns 0. */
 int rt_debug_last_split(long long out[3]);
+/* RT_DEBUG_TIMERS builds: per wave of the last analytic-scene megakernel launches (k_megakernel_f64), on the
+ * constant 100 MHz s_memrealtime clock: out[5w] its start, out[5w + 1] when fewer than half of its lanes
+ * last held work (all ones: never), out[5w + 2] its end (zeros: wave w did not run), and for the lane of it
+ * that ran out of work last: out[5w + 3] when it took its last unit, out[5w + 4] that unit (ticket); then
+ * cleared. For
+ * n_waves <= 8192. Returns 0, 1 without the timers (zeros), -1 on a HIP error. */
+int rt_debug_wave_times(unsigned long long* out, int n_waves);
 #ifdef __cplusplus
 }
 #endif

@@ -61,6 +61,15 @@ __device__ __forceinline__ void flush_count(unsigned long long* counter, uint32_
     if (__lane_id() == 0 && v) atomicAdd(counter, v);
     n = 0;
 }
+// flush_count when a lane's 32-bit count nears overflow (at a unit switch, `done`): the per-lane counts of a
+// launch stay far below 2^30 (a lane traces ~10^5 to 10^6 vertices), so in practice once, at the kernel's end.
+// (Flushing at every unit switch put a second device-scope atomic on one address next to each ticket, in every
+// render with stats: with 1.5 subpixels per lane split into 32-sample chunks, an N = 8 cornell share ran at 1688.7
+// Msamples/s with it and 1903.4 without, profiles/r06s_ab_tail_share.log / r06u_ab_tail.log.)
+constexpr uint32_t kFlushAt = 1u << 30;
+__device__ __forceinline__ void flush_count_if_full(unsigned long long* counter, uint32_t& n, bool done) {
+    if (__any(done && n >= kFlushAt)) flush_count(counter, n);
+}
 
 // Work unit of ticket t: the whole subpixels [id, end) (t < n_wunits: a run of unit_subs consecutive
 // subpixels, samples [0, n) each), or chunk c = t - n_wunits of the split tail (subpixel
@@ -293,9 +302,18 @@ static inline void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_
 // subpixel's sub_buf entry; every later chunk stores each sample's radiance for k_tail_sum_f64, which
 // continues the same sequential sum from chunk 0's partial (the same bits as one lane summing all).
 __device__ __forceinline__ bool tail_in_place(const RenderArgs& a, int s) { return (s >> a.chunk_lg) == 0; }
+#ifndef RT_TAIL_PROBE
+#define RT_TAIL_PROBE 0  // diagnostic builds only: 1 = every lane stores to one slot of its own (wrong frames; the
+                         // per-sample stores' footprint without their scatter)
+#endif
 __device__ __forceinline__ double* tail_slot(const RenderArgs& a, int id, int s) {
+#if RT_TAIL_PROBE == 1
+    (void)id; (void)s;
+    return a.tail_buf + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 3;
+#else
     const int c0 = 1 << a.chunk_lg;
     return a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)(a.n_samples - c0) + (size_t)(s - c0)) * 3;
+#endif
 }
 
 // k_tail_sum_f64 for the split tail of a megakernel launch (render_f64.hip)

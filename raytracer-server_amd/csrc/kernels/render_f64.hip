@@ -36,6 +36,15 @@ typedef __attribute__((address_space(3))) uint64_t LdsU64;
 #define RT_OPT_COLD 1  // A/B: mirror-bounce state (o, pre-bounce throughput) in LDS (LdsCold) or registers
 #endif
 
+// Diagnostic builds (RT_DEBUG_TIMERS): each wave of k_megakernel_f64 records, on the constant 100 MHz clock
+// (s_memrealtime), when it started, when fewer than half of its lanes last held work (-1: never), and when it
+// ended (rt_debug_wave_times, tools/end_probe.py --waves): the end phase of a launch, wave by wave.
+#if RT_DEBUG_TIMERS
+constexpr int kDbgWaves = 8192;
+constexpr int kDbgWaveRec = 5;
+__device__ unsigned long long g_dbg_wave[kDbgWaveRec * kDbgWaves];
+#endif
+
 template <int F, int W>
 __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, RenderArgs a_g, double* __restrict__ sub_buf,
                                                           uint32_t* next_sub, long nsub, int refill) {
@@ -82,7 +91,17 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
     PathState ps;
     bool fresh = true;
     int nbuf = 0, hb = 0;  // buffered camera samples (s + 1 .. s + nbuf) and the ring's head slot
+#if RT_DEBUG_TIMERS
+    const unsigned long long w_t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long w_half = ~0ull;
+    // per lane: when it took the unit it holds (l_take, l_unit) and when it ran out of work (l_end)
+    unsigned long long l_take = w_t0, l_end = w_t0;
+    long l_unit = t0;
+#endif
     while (__any(active)) {
+#if RT_DEBUG_TIMERS
+        if (w_half == ~0ull && __popcll(__ballot(active)) < 32) w_half = __builtin_amdgcn_s_memrealtime();
+#endif
         RT_DBG_REGION(0);
         RT_DBG_TSTART(t_it);
         bool done = false;
@@ -183,7 +202,18 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
         bool stop = false;
         if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
         const long nt = wave_ticket(next_sub, done && !stop);
-        if (__any(done)) flush_count(a.counters, nverts);  // keeps the 32-bit lane counts far from overflow
+        flush_count_if_full(a.counters, nverts, done);
+#if RT_DEBUG_TIMERS
+        if (done) {
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            if (nt < nunits) {
+                l_take = now;
+                l_unit = nt;
+            } else {
+                l_end = now;
+            }
+        }
+#endif
         if (done) {
             int end_unused;
             unit_of(a, nt, id, end_unused, s);
@@ -197,6 +227,32 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
         RT_DBG_TEND(0, t_it);
     }
     flush_count(a.counters, nverts);
+#if RT_DEBUG_TIMERS
+    {
+        const unsigned long long w_t1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        // the lane that ran out of work last: when it took its last unit, and which
+        unsigned long long e = l_end, tk = l_take;
+        long u = l_unit;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long e2 = __shfl_xor(e, off, 64), tk2 = __shfl_xor(tk, off, 64);
+            const long u2 = __shfl_xor(u, off, 64);
+            const bool take2 = e2 > e || (e2 == e && u2 > u);
+            e = take2 ? e2 : e;
+            tk = take2 ? tk2 : tk;
+            u = take2 ? u2 : u;
+        }
+        if ((threadIdx.x & 63) == 0 && wid < (unsigned)kDbgWaves) {
+            unsigned long long* r = g_dbg_wave + kDbgWaveRec * wid;
+            r[0] = w_t0;
+            r[1] = w_half;
+            r[2] = w_t1;
+            r[3] = tk;
+            r[4] = (unsigned long long)u;
+        }
+    }
+#endif
     RT_DBG_TFLUSH();
 }
 
@@ -263,7 +319,7 @@ static void launch_mk(const DevScene& sc, const RenderArgs& a_in, double* sub_bu
                       int refill, double* tail_buf, size_t tail_cap, hipStream_t st) {
     const long blocks = resident_blocks(k_megakernel_f64<F, W>, (nsub + 255) / 256);
     RenderArgs a = a_in;
-    plan_tail(a, nsub, blocks * 256, tail_buf, tail_cap);
+    plan_tail(a, nsub, blocks * 256, tail_buf, tail_cap, tail_split_x2(nsub, blocks * 256));
     hipLaunchKernelGGL((k_megakernel_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub, nsub,
                        refill);
     const long n_split = nsub - a.n_whole;
@@ -407,6 +463,22 @@ __global__ void k_selftest_arith(long n, uint64_t seed, unsigned long long* bad)
     if (e & 1) atomicAdd(&bad[0], 1ull);
     if (e & 2) atomicAdd(&bad[1], 1ull);
     if (e & 4) atomicAdd(&bad[2], 1ull);
+}
+
+// Diagnostic builds: the wave records of the last k_megakernel_f64 launches (start, half-idle, end per wave, on
+// the 100 MHz s_memrealtime clock; zeros for waves that did not run), then cleared; 1 (zeros) without timers.
+extern "C" int rt_debug_wave_times(unsigned long long* out, int n_waves) {
+    if (!out || n_waves <= 0) return -1;
+    for (long i = 0; i < 5L * n_waves; ++i) out[i] = 0;
+#if RT_DEBUG_TIMERS
+    const int n = std::min(n_waves, kDbgWaves);
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_wave), kDbgWaveRec * sizeof(unsigned long long) * n) != hipSuccess) return -1;
+    static unsigned long long zeros[kDbgWaveRec * kDbgWaves];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_wave), zeros, sizeof zeros) != hipSuccess) return -1;
+    return 0;
+#else
+    return 1;
+#endif
 }
 
 // The split tail of the calling thread's last megakernel launch (kernels.h TailPlan).

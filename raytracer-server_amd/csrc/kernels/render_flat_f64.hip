@@ -505,7 +505,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
         bool stop = false;
         if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
         const long nt = wave_ticket(next_sub, done && !stop);
-        if (__any(done)) flush_count(a.counters, nverts);
+        flush_count_if_full(a.counters, nverts, done);
         bool ended = false;
         if (done) {
             unit_of(a, nt, id, end, s);
@@ -797,7 +797,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
         bool stop = false;
         if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
         const long nt = wave_ticket(next_sub, done && !stop);
-        if (__any(done)) flush_count(a.counters, nverts);
+        flush_count_if_full(a.counters, nverts, done);
         if (done) {
             unit_of(a, nt, id, end, s);
             active = !stop && nt < nunits;
@@ -864,7 +864,7 @@ template <int F, int W, int B = kBlk>
 static void launch_fpool(const DevScene& sc, RenderArgs& a, double* sub_buf, uint32_t* next_sub, long nsub,
                          double* tail_buf, size_t tail_cap, int pool_min, int refill, hipStream_t st) {
     const long blocks = resident_blocks(k_megakernel_fpool_f64<F, W, B>, (nsub + B - 1) / B, B);
-    plan_tail(a, nsub, blocks * B, tail_buf, tail_cap);
+    plan_tail(a, nsub, blocks * B, tail_buf, tail_cap, tail_split_x2(nsub, blocks * B));
     hipLaunchKernelGGL((k_megakernel_fpool_f64<F, W, B>), dim3((unsigned)blocks), dim3(B), 0, st, sc, a, sub_buf,
                        next_sub, nsub, pool_min, refill);
 }

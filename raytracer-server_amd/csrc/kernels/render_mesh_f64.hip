@@ -788,7 +788,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
         bool stop = false;
         if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
         const long nt = wave_ticket(next_sub, done && !stop);
-        if (__any(done)) flush_count(a.counters, nverts);  // keeps the 32-bit lane counts far from overflow
+        flush_count_if_full(a.counters, nverts, done);
         if (done) {
             unit_of(a, nt, id, end, s);
             active = !stop && nt < nunits;
@@ -1200,7 +1200,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
             bool stop = false;
             if (a.cancel && __any(done)) stop = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
             const long nt = wave_ticket(next_sub, done && !stop);
-            if (__any(done)) flush_count(a.counters, nverts);
+            flush_count_if_full(a.counters, nverts, done);
             bool retire = false;
             if (done) {
                 int end_unused;

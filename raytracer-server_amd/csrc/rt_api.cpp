@@ -1062,17 +1062,22 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
         if (e == hipSuccess) {
             a.counters = ps ? ws->counters : nullptr;
             // split-tail scratch (megakernel_common.h plan_tail): the samples after chunk 0 of the subpixels a
-            // launch splits — half a subpixel per resident lane in the analytic and flat-mesh kernels (no more
-            // than 1024 lanes per CU: 4 waves/SIMD, the 1024-thread query pool), so 512 per CU (2^17 on 256
-            // CUs: 704 MB at 1024 spp); six per path slot in the mesh walk kernels (<= 1024 slots per CU) —
-            // at most 1.5 GB. A smaller buffer only splits fewer subpixels (plan_tail), with the same frame bits.
+            // launch splits — kernels.h tail_split_x2 / 2 per resident lane in the analytic and flat-mesh kernels
+            // (no more than 1024 lanes per CU: 4 waves/SIMD, the 1024-thread query pool), so 512 per CU (2^17 on
+            // 256 CUs: 704 MB at 1024 spp), 1536 for frames of <= 8 subpixels per lane; six per path slot in the
+            // mesh walk kernels (<= 1024 slots per CU) — at most 3 GB. A smaller buffer only splits fewer
+            // subpixels (plan_tail; rt_debug_last_split reports the split wanted and made), with the same frame bits.
             const bool walk = (a.features & 1) && !a.all_flat;
             int dev = 0, ncu = 256;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
             const size_t per_sub = rt::tail_scratch_per_subpixel(a.n_samples);
-            const size_t per_cu = walk ? 6 * 1024 : 512;
-            const size_t want = std::min<size_t>((size_t)3 << 29, per_sub * std::min<size_t>(npix * 4, (size_t)std::max(ncu, 1) * per_cu));
+            // (A/B builds: RT_MK_TAIL_SCRATCH_PER_CU / RT_MK_TAIL_SCRATCH_MB override both bounds, ab_knobs.h)
+            const long ncu_lanes = (long)std::max(ncu, 1) * 1024;
+            const size_t per_cu = (size_t)rt::ab_knob("RT_MK_TAIL_SCRATCH_PER_CU",
+                                                      walk ? 6 * 1024 : 512 * rt::tail_split_x2((long)npix * 4, ncu_lanes));
+            const size_t cap = (size_t)rt::ab_knob("RT_MK_TAIL_SCRATCH_MB", 3072) << 20;
+            const size_t want = std::min<size_t>(cap, per_sub * std::min<size_t>(npix * 4, (size_t)std::max(ncu, 1) * per_cu));
             if (!fp32 && per_sub > 0 && want >= per_sub) {
                 if (ws->ensure_tail(want) != hipSuccess) (void)hipGetLastError();  // no tail split then
             }

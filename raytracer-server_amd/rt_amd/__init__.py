@@ -118,6 +118,8 @@ def _load():
         L.rt_debug_counters.argtypes = [P(ctypes.c_ulonglong)]
     if hasattr(L, "rt_debug_regions"):
         L.rt_debug_regions.argtypes = [P(ctypes.c_ulonglong)]
+    if hasattr(L, "rt_debug_wave_times"):
+        L.rt_debug_wave_times.argtypes = [P(ctypes.c_ulonglong), ctypes.c_int]
     if hasattr(L, "rt_debug_last_split"):
         L.rt_debug_last_split.argtypes = [P(ctypes.c_longlong)]
     return L

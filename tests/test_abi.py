@@ -27,7 +27,8 @@ def test_exports_diagnostics(rt):
     text = open(os.path.join(REPO, "include", "rt_diag.h")).read()
     names = re.findall(r"^int\s+(rt_[a-z_0-9]+)\s*\(", text, re.M)
     assert names == ["rt_selftest_arith_n", "rt_selftest_arith", "rt_selftest_tables", "rt_debug_qcheck",
-                     "rt_debug_counters", "rt_debug_regions", "rt_debug_last_split"]
+                     "rt_debug_counters", "rt_debug_regions", "rt_debug_last_split",
+                     "rt_debug_wave_times"]
     for n in names:
         assert hasattr(rt.lib, n), f"missing export {n}"
     assert rt.debug_qcheck() is None  # the product library is built without the protocol checks

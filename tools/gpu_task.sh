@@ -9,6 +9,8 @@
 #   rehearse[:N]     the N-rank bench path (default 2) on this one GPU: torchrun, every rank on GPU 0
 #                    (RT_BENCH_DEVICE=0), 1 step; its frame_sha1 must equal N = 1's
 #   trace            rocprofv3 --kernel-trace --stats of `python bench.py --no-cpu-baseline`
+#   ktrace:SCRIPT[:ARGS]  rocprofv3 --kernel-trace --stats of `python SCRIPT ARGS` (":" separates args);
+#                    per-kernel totals -> $OUT/ktrace_<n>/run_kernel_stats.csv
 #   benchpmc         counter passes over `bench.py --steps 1 --warmup 0`: HBM bytes -> $OUT/pmc_traffic.json,
 #                    VALU mix + clock -> $OUT/pmc_valu.json (bench.py roofline.traffic / .compute)
 #   configs          tools/configs_bench.py (every BASELINE config, one GPU)
@@ -26,6 +28,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-run}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
+KT=0
 
 fail() { echo "FAIL: $1"; [ -f "$2" ] && tail -30 "$2"; exit 1; }
 
@@ -71,6 +74,13 @@ for task in "$@"; do
         timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
             python bench.py --no-cpu-baseline $BENCH_ARGS > "$OUT/trace.log" 2>&1 || fail trace "$OUT/trace.log"
         tail -1 "$OUT/trace.log" | cut -c1-300 ;;
+    ktrace)
+        script=${A[1]}
+        KT=$((KT + 1))
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/ktrace_$KT" -o run --output-format csv -- \
+            python "$script" "${A[@]:2}" > "$OUT/ktrace_$KT.log" 2>&1 || fail ktrace "$OUT/ktrace_$KT.log"
+        tail -1 "$OUT/ktrace_$KT.log" | cut -c1-300
+        find "$OUT/ktrace_$KT" -name "*kernel_stats.csv" -exec cut -d, -f1-5 {} \; | head -8 ;;
     benchpmc)
         # the bench command's own counters: HBM traffic (roofline.traffic; separate FETCH / WRITE passes)
         # and the VALU instruction mix + clock (roofline.compute), each pass a run of its own
