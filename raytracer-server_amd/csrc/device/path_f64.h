@@ -1271,8 +1271,15 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         if (Hoist != 0 && open) {
 #pragma unroll
             for (int j = 0; j < kTrisPerStep; ++j) {
+#if RT_LTRI_INDEX
+                // leaf lists as triangle ids only (no ltris uploaded): the triangle from the 3.6 MB table, one
+                // dependent load later (round 6: C4 -2.2%, C5 -3.7% against the copies, profiles/r06aa_ab_oct_ltidx.log)
+                tid[j] = sc.ltri_id[min(w.lpos + j, w.lend - 1)];
+                tr[j] = sc.tris[tid[j]];
+#else
                 tr[j] = sc.ltris[min(w.lpos + j, w.lend - 1)];
                 if (RT_LTRI_ID_HOIST) tid[j] = sc.ltri_id[min(w.lpos + j, w.lend - 1)];
+#endif
             }
         }
         SlotPF pf;
@@ -1284,7 +1291,7 @@ RT_DEV int walk_step(const DevScene& sc, const DevMesh& m, const Ray& ray, const
         }
         RT_DBG_TSTART(t_lt);
         if (Hoist != 0 ? open : w.lpos < w.lend) {
-            const int st = Hoist != 0 ? leaf_tris_loaded(sc, ray, w, tr, t, prim, RT_LTRI_ID_HOIST ? tid : nullptr)
+            const int st = Hoist != 0 ? leaf_tris_loaded(sc, ray, w, tr, t, prim, (RT_LTRI_ID_HOIST || RT_LTRI_INDEX) ? tid : nullptr)
                                       : leaf_tris(sc, ray, w, t, prim);
             if (st == WALK_HIT) {
                 RT_DBG_TEND(12, t_lt);
