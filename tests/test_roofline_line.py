@@ -14,7 +14,7 @@ sys.path.insert(0, REPO)
 import bench  # noqa: E402
 
 HEAD_KEY = "cornell_box 1920x1080x1024spp megakernel"
-VERTICES = 31305285173  # BENCH_r05.json config.vertices
+VERTICES = 31305285173  # BENCH_r05.json config.vertices (the same frame every round)
 SAMPLES = 1920 * 1080 * 1024
 KERNEL_MS = 1062.826  # BENCH_r05.json roofline.kernel_ms
 

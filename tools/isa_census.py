@@ -24,7 +24,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = "/opt/rocm/lib/llvm/bin"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=gfx950", "-munsafe-fp-atomics",
          "-gline-tables-only", "--cuda-device-only", "-c"]
-FN_DEF = re.compile(r"^(?:template\s*<[^>]*>\s*)?(?:RT_DEV|__device__|static|__global__|inline|\w+\s)[^;{]*?\b(\w+)\s*\([^;]*$")
+# a function definition starts at column 0 (its body is indented): the last identifier before the first "("
+# (or, inside a struct, at an indent of at most 4 with RT_DEV: a member function)
+FN_DEF = re.compile(r"^(?:template\s*<[^>]*>\s*)?[A-Za-z_][\w:<>,*&\s]*?\b(\w+)\s*\(|^ {1,4}(?:static\s+)?RT_DEV\b[\w:<>,*&\s]*?\b(\w+)\s*\(")
 
 
 def disasm(src, extra):
@@ -52,8 +54,10 @@ def function_of(path, line):
         cur = "?"
         for i, text in enumerate(lines, 1):
             m = FN_DEF.match(text)
-            if m and m.group(1) not in ("if", "for", "while", "switch", "return", "sizeof"):
-                cur = m.group(1)
+            name = (m.group(1) or m.group(2)) if m else None
+            if m and name not in ("if", "for", "while", "switch", "return", "sizeof", "defined", "static_assert",
+                                        "__attribute__", "typedef", "enum", "struct", "template"):
+                cur = name
             names.append(cur)
         _fn_cache[path] = names
     names = _fn_cache[path]
