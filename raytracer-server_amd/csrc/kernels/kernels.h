@@ -43,15 +43,18 @@ struct TailPlan {
     long n_split = 0, want = 0, chunk = 0;
 };
 extern thread_local TailPlan t_tail_plan;
-// Subpixels the analytic and flat-mesh megakernels split per resident lane, x2 (plan_tail's split_x2): half a
-// subpixel per lane for frames of more than 8 subpixels per lane, one and a half for up to 8 (an N = 4 rank share
-// of a frame), two for up to 4 (N = 8). The tail's chunks must outlast the last whole subpixels, and a subpixel
-// can cost 1.35x the average (its paths' lengths): in a share of ~4 subpixels per lane the last whole ones started
-// at 2/3 of the launch and ended 6 ms after every other wave (profiles/r06h_end_probe_waves.log). Cornell N = 8
-// share: 1864.6 (0.5 per lane) -> 1903.4 (1.5, profiles/r06u_ab_tail.log) -> 1909.1 (2; 2.5: 1910.7,
-// profiles/r06y_ab_tail_n8.log) Msamples/s; cubes 994.2 -> 1052.7 at 1.5 (profiles/r06v_ab_tail_roles.log).
+// Subpixels the analytic and flat-mesh megakernels split per resident lane, x2 (plan_tail's split_x2): one and a
+// half per lane, two for frames of up to 4 subpixels per lane (an N = 8 rank share). The tail's chunks must outlast
+// the last whole subpixels, and a subpixel can cost 1.35x the average (its paths' lengths): in a share of ~4
+// subpixels per lane the last whole ones started at 2/3 of the launch and ended 6 ms after every other wave
+// (profiles/r06h_end_probe_waves.log); in the full cornell frame with half a subpixel per lane split, the last
+// waves ended 15 ms after the median one, each behind a whole subpixel taken 59 ms before its end
+// (profiles/r06ah_end_probe_waves.log). Cornell N = 8 share: 1864.6 (0.5 per lane) -> 1903.4 (1.5,
+// profiles/r06u_ab_tail.log) -> 1909.1 (2; 2.5: 1910.7, profiles/r06y_ab_tail_n8.log) Msamples/s; full frames at
+// 0.5 -> 1.5 per lane: cornell 1988.3 -> 2003.8 (2: 2001.2, profiles/r06ai_ab_tail_full.log), cubes 1079.5 -> 1085.5,
+// N = 2 shares cornell 1963.9 -> 1987.8 and cubes 1067.5 -> 1079.7 (profiles/r06aj_ab_tail_full.log).
 // rt_api.cpp sizes the split-tail scratch with the same rule.
-inline int tail_split_x2(long nsub, long lanes) { return nsub <= 4 * lanes ? 4 : nsub <= 8 * lanes ? 3 : 1; }
+inline int tail_split_x2(long nsub, long lanes) { return nsub <= 4 * lanes ? 4 : 3; }
 // Split-tail scratch bytes per split subpixel (megakernel_common.h plan_tail: the samples after chunk 0).
 size_t tail_scratch_per_subpixel(int n_samples);
 // tail_buf / tail_cap: scratch for the split tail (bytes); the launcher sizes the tail to fit it.

@@ -259,9 +259,9 @@ static inline void plan_units(RenderArgs& a, long lanes) {
     a.n_wunits = (int32_t)(((long)a.n_whole + b - 1) / b);
 }
 
-// split_x2 = 1 (half a subpixel per lane, cap_div 2: at most half the frame): the analytic and flat-mesh
-// kernels, whose subpixels cost about the same, so two chunks per lane at the frame's end balance it
-// (one subpixel per lane measured no better, profiles/r05ae_tail_probe_cornell1024.log). The mesh walk
+// split_x2 / 2 subpixels per resident lane, cap_div 2 (at most half the frame): the analytic and flat-mesh
+// kernels pass kernels.h tail_split_x2 (1.5 per lane, 2 in frames of <= 4 per lane; the default 1 is half a
+// subpixel per lane, the round-5 rule, which left the full frame's last waves behind whole subpixels). The mesh walk
 // kernels pass 12 and 1 (six subpixels per path slot, up to the whole frame): a unicorn subpixel's cost
 // depends on where it lies (walls or the mesh), and the last whole subpixels' spread left an N = 8 share
 // at 0.81 of the full frame's rate with half a subpixel per slot, 0.96 with six (profiles/r05bc_tail.log).

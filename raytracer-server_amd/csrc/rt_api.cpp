@@ -1063,8 +1063,8 @@ int render_enqueue(rt_scene* s, const rt_render_params* p, uint8_t* d_rgb, doubl
             a.counters = ps ? ws->counters : nullptr;
             // split-tail scratch (megakernel_common.h plan_tail): the samples after chunk 0 of the subpixels a
             // launch splits — kernels.h tail_split_x2 / 2 per resident lane in the analytic and flat-mesh kernels
-            // (no more than 1024 lanes per CU: 4 waves/SIMD, the 1024-thread query pool), so 512 per CU (2^17 on
-            // 256 CUs: 704 MB at 1024 spp), 1536 / 2048 for frames of <= 8 / 4 subpixels per lane; six per path slot in the
+            // (no more than 1024 lanes per CU: 4 waves/SIMD, the 1024-thread query pool), so 1536 per CU (393,216 on
+            // 256 CUs: 2.1 GB at 1024 spp), 2048 for frames of <= 4 subpixels per lane; six per path slot in the
             // mesh walk kernels (<= 1024 slots per CU) — at most 3 GB. A smaller buffer only splits fewer
             // subpixels (plan_tail; rt_debug_last_split reports the split wanted and made), with the same frame bits.
             const bool walk = (a.features & 1) && !a.all_flat;

@@ -1,5 +1,6 @@
 """Diagnostic: lane utilisation per instrumented region of the megakernel (RT_DEBUG_COUNTERS build).
-python tools/dbg_regions.py <lib.so> SCENE W H SPP"""
+python tools/dbg_regions.py <lib.so> SCENE W H SPP [share=N/R]  (share: rank R's interleaved rows of N, bench.py's
+partition)"""
 import ctypes, os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["RT_AMD_LIB"] = sys.argv[1]
@@ -13,10 +14,15 @@ scene, w, h, spp = sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv
 s = rt_amd.Scene.from_toml(os.path.join(REPO, "scenes", f"{scene}.toml"))
 c = (ctypes.c_ulonglong * 64)()
 rt_amd.lib.rt_debug_regions(c)
-rgb, _, st = rt_amd.render(s, w, h, spp, megakernel=True)
+kw = {}
+share = next((x for x in sys.argv[6:] if x.startswith("share=")), None)
+if share:
+    sn, sr = (int(v) for v in share[6:].split("/"))
+    kw = dict(tile=(0, sr, w, (h - sr + sn - 1) // sn), row_step=sn)
+rgb, _, st = rt_amd.render(s, w, h, spp, megakernel=True, **kw)
 rt_amd.lib.rt_debug_regions(c)
 it = max(1, c[0])
-print(f"{scene} {w}x{h}x{spp}: vertices {st['vertices']}, wave iterations {c[0]}")
+print(f"{scene} {w}x{h}x{spp}{' ' + share if share else ''}: vertices {st['vertices']}, wave iterations {c[0]}")
 TNAMES = {0: "iteration", 1: "fresh block", 2: "trace_closest (main)", 3: "shade_vertex", 4: "refill pass",
           5: "bookkeeping (ticket/cancel)", 6: "sample-end block", 7: "surface()", 9: "light_sample", 10: "visible()",
           11: "brdf_sample", 13: "trace: inv + axis planes", 14: "trace: spheres"}
