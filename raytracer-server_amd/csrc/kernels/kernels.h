@@ -19,7 +19,8 @@ struct RenderArgs {
     int32_t tail_cps;    // split tail: chunks per subpixel
     // split tail (megakernels): subpixels [n_whole, nsub) are handed out as chunks of 2^chunk_lg
     // samples; a chunk's lane stores each sample's radiance in tail_buf[sub - n_whole][sample][3]
-    // and k_tail_sum adds them up in sample order afterwards (the same sequential sum)
+    // (megakernel_common.h tail_store) and k_tail_sum adds them up in sample order afterwards (the same
+    // sequential sum)
     int32_t n_whole, chunk_lg;
     // whole subpixels are handed out in runs of unit_subs consecutive subpixels per ticket (n_wunits
     // tickets): at low spp a ticket per subpixel makes the one global counter's atomics the bottleneck

@@ -285,7 +285,7 @@ static inline void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_
     a.chunk_lg = min_lg;
     while ((a.n_samples >> a.chunk_lg) > cps_target) ++a.chunk_lg;
     a.tail_cps = (a.n_samples + (1 << a.chunk_lg) - 1) >> a.chunk_lg;
-    // chunk 0 of a split subpixel sums in place (tail_stores): scratch only for the samples after it
+    // chunk 0 of a split subpixel sums in place (tail_in_place): scratch only for the samples after it
     const size_t per_sub = (size_t)std::max(0, a.n_samples - (1 << a.chunk_lg)) * 3 * sizeof(double);
     long n_split = 0, want = 0;
     if (tail_env && a.n_samples >= 64 && a.tail_cps >= 2 && per_sub > 0) {
@@ -306,14 +306,20 @@ __device__ __forceinline__ bool tail_in_place(const RenderArgs& a, int s) { retu
 #define RT_TAIL_PROBE 0  // diagnostic builds only: 1 = every lane stores to one slot of its own (wrong frames; the
                          // per-sample stores' footprint without their scatter)
 #endif
-__device__ __forceinline__ double* tail_slot(const RenderArgs& a, int id, int s) {
+// tail_buf layout: subpixel-major, [j][s - c0][3] (j = id - n_whole): a chunk's lane writes one contiguous run.
+// (Groups of 64 subpixels, sample-major with a row per component, made k_tail_sum's loads contiguous, 1.0 -> 0.46 ms
+// at N = 8, but scattered these stores: the frame ran 0.1-0.3% slower, profiles/r06an_ab_tail_layout.log.)
+__device__ __forceinline__ void tail_store(const RenderArgs& a, int id, int s, const f64::V3& L) {
 #if RT_TAIL_PROBE == 1
     (void)id; (void)s;
-    return a.tail_buf + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 3;
+    double* o = a.tail_buf + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 3;
 #else
     const int c0 = 1 << a.chunk_lg;
-    return a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)(a.n_samples - c0) + (size_t)(s - c0)) * 3;
+    double* o = a.tail_buf + ((size_t)(id - a.n_whole) * (size_t)(a.n_samples - c0) + (size_t)(s - c0)) * 3;
 #endif
+    o[0] = L.x;
+    o[1] = L.y;
+    o[2] = L.z;
 }
 
 // k_tail_sum_f64 for the split tail of a megakernel launch (render_f64.hip)

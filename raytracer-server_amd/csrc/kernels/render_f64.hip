@@ -186,10 +186,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
                     }
                     ++s;
                 } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
-                    double* o = tail_slot(a, id, s);
-                    o[0] = ps.L.x;
-                    o[1] = ps.L.y;
-                    o[2] = ps.L.z;
+                    tail_store(a, id, s, ps.L);
                     done = !unit_has_next(a, id, s);
                     ++s;
                 }
@@ -259,20 +256,63 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
 // Split tail: subpixel n_whole + j's mean, continuing the sequential sum chunk 0 left in sub_buf (its lane
 // summed samples [0, c0) in place, megakernel_common.h tail_in_place) over the later chunks' stored sample
 // radiance, in sample order, with the same acc + L * inv_n expression as the megakernel's accumulator
-// (server.rs:357-358): the bits of one lane summing every sample. tail_buf is subpixel-major
-// ([j][sample - c0][3]): a chunk's lane writes one contiguous run (the sample-major layout scattered
-// every write over the whole buffer: TLB misses, 2x slower tail).
+// (server.rs:357-358): the bits of one lane summing every sample. A thread per subpixel; tail_buf is
+// subpixel-major (tail_store), so the block stages kTailStage samples of its 256 subpixels through LDS: the
+// staging loads read each subpixel's 192-byte run with 16-byte lanes side by side (a thread reading its own run
+// put every lane of a load on a line of its own: 2.8 GB in 1.0 ms at N = 8,
+// profiles/r06af_ktrace_share8_kernel_stats.csv; staged: 0.68 ms, profiles/r06ap_ktrace_share8_kernel_stats.csv,
+// the frame's kernel unchanged; a layout with contiguous reads, 0.46 ms, cost the megakernel's stores more, tail_store). LDS rows of kTailRow doubles (an odd count: the threads' 8-byte
+// reads spread over the banks).
+constexpr int kTailStage = 8, kTailRow = kTailStage * 3 + 1;
 __global__ __launch_bounds__(256) void k_tail_sum_f64(RenderArgs a, double* __restrict__ sub_buf, long n_split) {
-    const long stride = (long)gridDim.x * blockDim.x;
+    __shared__ double stage[256 * kTailRow];
     const int c0 = 1 << a.chunk_lg;
-    for (long j = (long)blockIdx.x * blockDim.x + threadIdx.x; j < n_split; j += stride) {
+    const int ns = a.n_samples - c0;
+    const size_t run = (size_t)ns * 3;  // doubles per subpixel in tail_buf
+    for (long base = (long)blockIdx.x * 256; base < n_split; base += (long)gridDim.x * 256) {
+        const long j = base + threadIdx.x;
+        const int nj = (int)min(256L, n_split - base);  // this block's subpixels
         double* o = sub_buf + (size_t)(a.n_whole + j) * 3;
-        V3 acc = v3(o[0], o[1], o[2]);
-        const double* L = a.tail_buf + (size_t)j * (size_t)(a.n_samples - c0) * 3;
-        for (int s = c0; s < a.n_samples; ++s, L += 3) acc = acc + v3(L[0], L[1], L[2]) * a.inv_n;
-        o[0] = acc.x;
-        o[1] = acc.y;
-        o[2] = acc.z;
+        V3 acc = j < n_split ? v3(o[0], o[1], o[2]) : v3(0, 0, 0);
+        const double* src = a.tail_buf + (size_t)base * run;
+        for (int s0 = 0; s0 < ns; s0 += kTailStage) {
+            const int nb = min(kTailStage, ns - s0);
+            __syncthreads();  // the previous stage's reads are done
+            if (nb == kTailStage && (run & 1) == 0) {
+                // 12 16-byte pieces per subpixel (runs and stages start 16-byte aligned: run and s0 * 3 even),
+                // 12 per thread: all loads issued before the LDS writes (one round trip per stage)
+                double2 v[12];
+#pragma unroll
+                for (int i = 0; i < 12; ++i) {
+                    const int e = threadIdx.x + 256 * i, q = e / 12, k = e - q * 12;
+                    if (q < nj) v[i] = *(const double2*)(src + (size_t)q * run + (size_t)s0 * 3 + 2 * k);
+                }
+#pragma unroll
+                for (int i = 0; i < 12; ++i) {
+                    const int e = threadIdx.x + 256 * i, q = e / 12, k = e - q * 12;
+                    if (q < nj) {
+                        stage[q * kTailRow + 2 * k] = v[i].x;
+                        stage[q * kTailRow + 2 * k + 1] = v[i].y;
+                    }
+                }
+            } else {
+                const int per = nb * 3;
+                for (int e = threadIdx.x; e < nj * per; e += 256) {
+                    const int q = e / per, k = e - q * per;
+                    stage[q * kTailRow + k] = src[(size_t)q * run + (size_t)s0 * 3 + k];
+                }
+            }
+            __syncthreads();
+            if (j < n_split) {
+                const double* r = stage + threadIdx.x * kTailRow;
+                for (int k = 0; k < nb; ++k) acc = acc + v3(r[3 * k], r[3 * k + 1], r[3 * k + 2]) * a.inv_n;
+            }
+        }
+        if (j < n_split) {
+            o[0] = acc.x;
+            o[1] = acc.y;
+            o[2] = acc.z;
+        }
     }
 }
 

@@ -494,10 +494,7 @@ __global__ __launch_bounds__(kBlk, W) void k_megakernel_flat_f64(DevScene sc_g, 
                 }
                 ++s;
             } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
-                double* o = tail_slot(a, id, s);
-                o[0] = ps.L.x;
-                o[1] = ps.L.y;
-                o[2] = ps.L.z;
+                tail_store(a, id, s, ps.L);
                 done = !unit_has_next(a, id, s);
                 ++s;
             }
@@ -786,10 +783,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
                     ++s;
                 }
             } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
-                double* o = tail_slot(a, id, s);
-                o[0] = ps.L.x;
-                o[1] = ps.L.y;
-                o[2] = ps.L.z;
+                tail_store(a, id, s, ps.L);
                 done = !unit_has_next(a, id, s);
                 ++s;
             }

@@ -627,10 +627,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
                     }
                     ++s;
                 } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
-                    double* o = tail_slot(a, id, s);
-                    o[0] = ps.L.x;
-                    o[1] = ps.L.y;
-                    o[2] = ps.L.z;
+                    tail_store(a, id, s, ps.L);
                     done = !unit_has_next(a, id, s);
                     ++s;
                 }
@@ -761,10 +758,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
                     }
                     ++s;
                 } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
-                    double* o = tail_slot(a, id, s);
-                    o[0] = ps.L.x;
-                    o[1] = ps.L.y;
-                    o[2] = ps.L.z;
+                    tail_store(a, id, s, ps.L);
                     done = !unit_has_next(a, id, s);
                     ++s;
                 }
@@ -1186,10 +1180,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
                             ++s;
                         }
                     } else {  // split tail, later chunks: each sample's radiance, summed in order by k_tail_sum_f64
-                        double* o = tail_slot(a, id, s);
-                        o[0] = ps.L.x;
-                        o[1] = ps.L.y;
-                        o[2] = ps.L.z;
+                        tail_store(a, id, s, ps.L);
                         done = !unit_has_next(a, id, s);
                         ++s;
                     }

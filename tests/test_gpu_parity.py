@@ -142,15 +142,18 @@ def test_split_tail_equals_wavefront(rt, gpu_scenes):
             assert a[2]["vertices"] == b[2]["vertices"]
 
 
-@pytest.mark.parametrize("name,mis", [("cornell_box", False), ("cubes", False), ("flying_unicorn", False),
-                                      ("chair_phong", True)])
-def test_split_tail_parity_against_oracle(name, mis, rt, gpu_scenes, oracle_scenes, oracle, tmp_path):
+@pytest.mark.parametrize("name,mis,spp", [("cornell_box", False, 256), ("cubes", False, 256),
+                                          ("flying_unicorn", False, 256), ("chair_phong", True, 256),
+                                          ("cornell_box", False, 308)])
+def test_split_tail_parity_against_oracle(name, mis, spp, rt, gpu_scenes, oracle_scenes, oracle, tmp_path):
     """The split tail of every megakernel family against the oracle (1e-9 / RGB8), at 256 spp (64 samples per
     subpixel: the smallest spp that splits, plan_tail): chunk 0 of a split subpixel sums in place in sub_buf,
     the later chunks store each sample's radiance at tail_slot, and k_tail_sum_f64 continues chunk 0's partial
     sum. cornell: the analytic kernel (half the frame split); cubes: the 1024-thread query pool; the unicorn:
     the role-split pool (the whole frame split, six subpixels per path slot); a Phong chair with MIS: the
-    512-thread Phong / MIS role-pool instance. The launch must have split subpixels (rt_debug_last_split)."""
+    512-thread Phong / MIS role-pool instance. 308 spp (77 samples per subpixel, 45 stored per split subpixel: an
+    odd run, a partial last stage) takes k_tail_sum_f64's generic staging path. The launch must have split
+    subpixels (rt_debug_last_split)."""
     if name == "chair_phong":
         from test_host_prep import extra_asset_scene
 
@@ -165,7 +168,7 @@ def test_split_tail_parity_against_oracle(name, mis, rt, gpu_scenes, oracle_scen
         sc, orc = rt.Scene.from_toml(p), oracle.OracleScene(p)
     else:
         sc, orc = gpu_scenes[name], oracle_scenes[name]
-    w, h, spp = 32, 24, 256
+    w, h = 32, 24
     tile = (0, 0, w, h) if name != "flying_unicorn" else None
     if name == "flying_unicorn":  # the mesh's part of the frame (a 32x24 crop of 640x480)
         w, h, tile = 640, 480, (300, 230, 32, 24)
