@@ -880,7 +880,9 @@ hipError_t launch_megakernel_flat_f64(const DevScene& sc, const RenderArgs& a_in
     RenderArgs a = a_in;
     static const int waves = env_int("RT_MK_FLAT_WAVES", 3);
     static const int fpool = env_int("RT_MK_FPOOL", 1);
-    static const int pool_min = env_int("RT_MK_FPOOL_MIN", 48);
+    // query chunks of pool_min (see RT_FPOOL_READY): 56 on the cubes 1024 spp 1093.3 Msamples/s (48: 1085.6, 64: 1087.6,
+    // 80: 1061.0, 96: 1037.1; MIS 1027.5 -> 1034.2 at 56; profiles/r06ar_ab_fpool_min.log, r06as_ab_fpool_min.log)
+    static const int pool_min = env_int("RT_MK_FPOOL_MIN", 56);
     static const int nospec = env_int("RT_MK_NOSPEC", 1);  // A/B: 0 = the mirror-capable kernel for every scene
     // camera-sample refill threshold of the query-pool kernel (no-mirror scenes): 16-24 lanes measured
     // best on the cubes (8: 736.9, 16: 747.2, 24: 745.2, 32: 737.3, 40: 730.9 Msamples/s; the analytic
