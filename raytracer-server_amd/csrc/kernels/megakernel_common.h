@@ -249,9 +249,13 @@ static inline int env_int(const char* name, int dflt) { return (int)ab_knob(name
 // RT_MK_UNITS_PER_LANE (16) runs per resident lane, so the frame's end stays balanced (2 runs per lane
 // left the unicorn's lanes idling behind a few long runs: -30%). At 1024 spp that is one subpixel per
 // ticket; at 64 spp (16 samples per subpixel) a ticket per subpixel put every wave behind the one
-// counter's atomic every few iterations (1920x1080x64: 2.3x the 1024-spp time per sample).
-static inline void plan_units(RenderArgs& a, long lanes) {
-    static const int target = std::max(1, env_int("RT_MK_UNIT_SAMPLES", 256));
+// counter's atomic every few iterations (1920x1080x64: 2.3x the 1024-spp time per sample). The mesh walk
+// kernels pass 64: their samples cost ~17x the analytic kernel's, so a run of 16 subpixels at 64 spp (C5) was
+// 1/21 of a path slot's frame and left slots idle behind the last runs: C5 363.0 -> 367.5 Msamples/s
+// (32: 368.0, 16: 368.5; profiles/r06av_ab_units_c5.log, r06aw_ab_units_c5.log), C4 unchanged.
+static inline void plan_units(RenderArgs& a, long lanes, int unit_samples = 256) {
+    static const int env_target = env_int("RT_MK_UNIT_SAMPLES", 0);
+    const int target = std::max(1, env_target > 0 ? env_target : unit_samples);
     static const int per_lane = std::max(1, env_int("RT_MK_UNITS_PER_LANE", 16));
     long b = std::max(1, target / std::max(1, a.n_samples));
     b = std::max(1L, std::min(b, (long)a.n_whole / std::max(1L, lanes * per_lane)));
@@ -266,7 +270,7 @@ static inline void plan_units(RenderArgs& a, long lanes) {
 // depends on where it lies (walls or the mesh), and the last whole subpixels' spread left an N = 8 share
 // at 0.81 of the full frame's rate with half a subpixel per slot, 0.96 with six (profiles/r05bc_tail.log).
 static inline void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_buf, size_t tail_cap, int split_x2 = 1,
-                             int cap_div = 2) {
+                             int cap_div = 2, int unit_samples = 256) {
     static const int tail_env = env_int("RT_MK_TAIL", 1);
     // A/B overrides: RT_MK_TAIL_MUL / RT_MK_TAIL_DIV subpixels per lane (defaults 1 / 2 once either is set),
     // RT_MK_TAIL_CAP_DIV, RT_MK_TAIL_MIN_LG (the shortest chunk, 2^min_lg samples)
@@ -295,7 +299,7 @@ static inline void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_
     if (nsub > 0) t_tail_plan = TailPlan{n_split, want, 1L << a.chunk_lg};  // rt_debug_last_split
     a.n_whole = (int32_t)(nsub - n_split);
     a.tail_buf = tail_buf;
-    plan_units(a, lanes);
+    plan_units(a, lanes, unit_samples);
 }
 // Split tail, per sample of a split subpixel: chunk 0 (samples [0, 2^chunk_lg)) sums its samples in
 // place, acc = acc + L * inv_n from 0 exactly like a whole subpixel, and leaves its partial sum in the

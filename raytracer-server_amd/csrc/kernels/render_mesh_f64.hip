@@ -1239,7 +1239,8 @@ static void launch_roles(const DevScene& sc, const RenderArgs& a_in, double* sub
     const long blocks = resident_blocks(k_megakernel_roles_f64<F, W, S>, (nsub + B - 1) / B, B);
     RenderArgs a = a_in;
     // the split tail and ticket runs planned for the lanes that hold paths (one path slot per thread)
-    plan_tail(a, nsub, blocks * RoleLayout<Cfg<F>>::paths, tail_buf, tail_cap, 12, 1);  // six subpixels per path slot
+    // six subpixels per path slot; runs of whole subpixels of ~64 samples (plan_units)
+    plan_tail(a, nsub, blocks * RoleLayout<Cfg<F>>::paths, tail_buf, tail_cap, 12, 1, 64);
     hipLaunchKernelGGL((k_megakernel_roles_f64<F, W, S>), dim3((unsigned)blocks), dim3(B), 0, st, sc, a, sub_buf, next_sub,
                        nsub);
     launch_tail_sum_f64(a, sub_buf, nsub - a.n_whole, st);
@@ -1252,7 +1253,7 @@ static void launch_mm(const DevScene& sc, const RenderArgs& a_in, double* sub_bu
     constexpr int B = P ? kPoolThreads : 256;
     const long blocks = resident_blocks(k_megakernel_mesh_f64<F, W, P, S>, (nsub + B - 1) / B, B);
     RenderArgs a = a_in;
-    plan_tail(a, nsub, blocks * B, tail_buf, tail_cap, 12, 1);
+    plan_tail(a, nsub, blocks * B, tail_buf, tail_cap, 12, 1, 64);
     hipLaunchKernelGGL((k_megakernel_mesh_f64<F, W, P, S>), dim3((unsigned)blocks), dim3(B), 0, st, sc, a, sub_buf,
                        next_sub, nsub, ksteps, wmin, refill, pool_min, pool_vmin);
     launch_tail_sum_f64(a, sub_buf, nsub - a.n_whole, st);
