@@ -32,6 +32,10 @@ typedef __attribute__((address_space(3))) uint64_t LdsU64;
 #ifndef RT_OPT_LDSOBJ
 #define RT_OPT_LDSOBJ 1  // A/B: the object table in LDS (per-lane object reads as ds_read)
 #endif
+#ifndef RT_MK_BEGIN_AT_END
+#define RT_MK_BEGIN_AT_END 1  // a lane whose sample ended starts its next buffered sample in the same divergent block
+#endif                        // (0: at the top of the next iteration, a block of its own; cornell 1024 spp 2000.6 ->
+                              // 2002.9, C2 MIS 1891.0 -> 1896.6, same frames: profiles/r06be_ab_begin_at_end.log)
 #ifndef RT_OPT_COLD
 #define RT_OPT_COLD 1  // A/B: mirror-bounce state (o, pre-bounce throughput) in LDS (LdsCold) or registers
 #endif
@@ -107,7 +111,7 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
         bool done = false;
         // camera: a lane starting a path takes its next buffered sample, or joins the camera pass
         RT_DBG_TSTART(t_fr);
-        if (active && fresh && nbuf > 0) {
+        if (!RT_MK_BEGIN_AT_END && active && fresh && nbuf > 0) {
             RT_DBG_REGION(2);
             const int q = hb * 3 * 256, r = hb * 2 * 256;
             begin_path(sc, CameraSample{v3(nbd[q], nbd[q + 256], nbd[q + 512]), nbr[r], nbr[r + 256]}, ps);
@@ -190,6 +194,17 @@ __global__ __launch_bounds__(256, W) void k_megakernel_f64(DevScene sc_g, Render
                     done = !unit_has_next(a, id, s);
                     ++s;
                 }
+#if RT_MK_BEGIN_AT_END
+                // the next sample of the same unit from the camera buffer, here rather than in a block of its own
+                // at the top of the next iteration (same lanes; the camera pass below sees the same ring state)
+                if (!done && nbuf > 0) {
+                    const int q = hb * 3 * 256, r = hb * 2 * 256;
+                    begin_path(sc, CameraSample{v3(nbd[q], nbd[q + 256], nbd[q + 512]), nbr[r], nbr[r + 256]}, ps);
+                    fresh = false;
+                    hb = hb + 1 == kCamDepth ? 0 : hb + 1;
+                    --nbuf;
+                }
+#endif
             }
             RT_DBG_TEND(6, t_se);
         }
