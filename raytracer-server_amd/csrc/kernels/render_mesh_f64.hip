@@ -824,7 +824,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_mesh_f64(DevScene sc_g, Ren
 #define RT_ROLES_REFILL 16  // a walker wave refills once at least this many of its lanes are idle
 #endif
 #ifndef RT_ROLES_PRIO
-#define RT_ROLES_PRIO 1  // walker waves at raised issue priority (their dependent loads issue first)
+#define RT_ROLES_PRIO 1  // walker waves at raised issue priority, this s_setprio level (their dependent loads issue first)
 #endif
 #ifndef RT_ROLES_BLOCK
 #define RT_ROLES_BLOCK 768  // threads of a block (one per CU: the path store takes the LDS): 3 waves/SIMD (168 VGPRs);
@@ -1012,7 +1012,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_roles_f64(DevScene sc_g, Re
         bool closest = false;
         WalkRegs r;
 #if RT_ROLES_PRIO
-        __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_s_setprio(RT_ROLES_PRIO);
 #endif
         for (;;) {
             RT_DBG_TSTART(t_wi);
