@@ -631,7 +631,7 @@ __global__ __launch_bounds__(B, W) void k_megakernel_fpool_f64(DevScene sc_g, Re
         RT_DBG_TSTART(t_q);
         // ---------------- (1) queued mesh queries, a chunk per mesh
 #if RT_FPOOL_PRIO
-        __builtin_amdgcn_s_setprio(1);  // A/B: the query chunks at raised issue priority
+        __builtin_amdgcn_s_setprio(RT_FPOOL_PRIO);  // A/B: the query chunks at raised issue priority (this level)
 #endif
         {
             const bool rdy = active && __hip_atomic_load(&s_pend[tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
