@@ -253,12 +253,20 @@ static inline int env_int(const char* name, int dflt) { return (int)ab_knob(name
 // kernels pass 64: their samples cost ~17x the analytic kernel's, so a run of 16 subpixels at 64 spp (C5) was
 // 1/21 of a path slot's frame and left slots idle behind the last runs: C5 363.0 -> 367.5 Msamples/s
 // (32: 368.0, 16: 368.5; profiles/r06av_ab_units_c5.log, r06aw_ab_units_c5.log), C4 unchanged.
-static inline void plan_units(RenderArgs& a, long lanes, int unit_samples = 256) {
+static inline void plan_units(RenderArgs& a, long lanes, int unit_samples = 256, int min_run = 1) {
     static const int env_target = env_int("RT_MK_UNIT_SAMPLES", 0);
     const int target = std::max(1, env_target > 0 ? env_target : unit_samples);
     static const int per_lane = std::max(1, env_int("RT_MK_UNITS_PER_LANE", 16));
-    long b = std::max(1, target / std::max(1, a.n_samples));
-    b = std::max(1L, std::min(b, (long)a.n_whole / std::max(1L, lanes * per_lane)));
+    // ... but, in the analytic kernel (min_run 32), never fewer than min_run samples per ticket while the frame has
+    // more than one run per lane: one counter word takes ~88 returning atomics per microsecond
+    // (MI355X_MICROARCH.md, "dequeue"), and a frame of a few samples per lane handed out a subpixel at a time is
+    // bound by it. C1' (600x450, 4 spp: one sample per subpixel) 291.5 -> 393.6 Msamples/s, cornell 1920x1080 at
+    // 64 spp 1570.6 -> 1808.7 (profiles/r06bo_ab_min_run.log; the kernel 3.70 -> 2.70 ms on C1',
+    // r06bn_ktrace_c1p_kernel_stats.csv); the cubes' query pool at 64 spp measured 1.9% slower with it (min_run 1).
+    const long n = std::max(1, a.n_samples), lanes1 = std::max(1L, lanes);
+    const long b_rate = std::min((std::max(1, min_run) + n - 1) / n, std::max(1L, (long)a.n_whole / lanes1));
+    long b = std::max(1L, target / n);
+    b = std::max(1L, std::min(b, std::max(b_rate, (long)a.n_whole / (lanes1 * per_lane))));
     a.unit_subs = (int32_t)b;
     a.n_wunits = (int32_t)(((long)a.n_whole + b - 1) / b);
 }
@@ -270,7 +278,7 @@ static inline void plan_units(RenderArgs& a, long lanes, int unit_samples = 256)
 // depends on where it lies (walls or the mesh), and the last whole subpixels' spread left an N = 8 share
 // at 0.81 of the full frame's rate with half a subpixel per slot, 0.96 with six (profiles/r05bc_tail.log).
 static inline void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_buf, size_t tail_cap, int split_x2 = 1,
-                             int cap_div = 2, int unit_samples = 256) {
+                             int cap_div = 2, int unit_samples = 256, int min_run = 1) {
     static const int tail_env = env_int("RT_MK_TAIL", 1);
     // A/B overrides: RT_MK_TAIL_MUL / RT_MK_TAIL_DIV subpixels per lane (defaults 1 / 2 once either is set),
     // RT_MK_TAIL_CAP_DIV, RT_MK_TAIL_MIN_LG (the shortest chunk, 2^min_lg samples)
@@ -299,7 +307,7 @@ static inline void plan_tail(RenderArgs& a, long nsub, long lanes, double* tail_
     if (nsub > 0) t_tail_plan = TailPlan{n_split, want, 1L << a.chunk_lg};  // rt_debug_last_split
     a.n_whole = (int32_t)(nsub - n_split);
     a.tail_buf = tail_buf;
-    plan_units(a, lanes, unit_samples);
+    plan_units(a, lanes, unit_samples, min_run);
 }
 // Split tail, per sample of a split subpixel: chunk 0 (samples [0, 2^chunk_lg)) sums its samples in
 // place, acc = acc + L * inv_n from 0 exactly like a whole subpixel, and leaves its partial sum in the

@@ -374,7 +374,7 @@ static void launch_mk(const DevScene& sc, const RenderArgs& a_in, double* sub_bu
                       int refill, double* tail_buf, size_t tail_cap, hipStream_t st) {
     const long blocks = resident_blocks(k_megakernel_f64<F, W>, (nsub + 255) / 256);
     RenderArgs a = a_in;
-    plan_tail(a, nsub, blocks * 256, tail_buf, tail_cap, tail_split_x2(nsub, blocks * 256));
+    plan_tail(a, nsub, blocks * 256, tail_buf, tail_cap, tail_split_x2(nsub, blocks * 256), 2, 256, 32);  // plan_units
     hipLaunchKernelGGL((k_megakernel_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub, nsub,
                        refill);
     const long n_split = nsub - a.n_whole;
