@@ -36,6 +36,10 @@ typedef __attribute__((address_space(3))) uint64_t LdsU64;
 #define RT_MK_BEGIN_AT_END 1  // a lane whose sample ended starts its next buffered sample in the same divergent block
 #endif                        // (0: at the top of the next iteration, a block of its own; cornell 1024 spp 2000.6 ->
                               // 2002.9, C2 MIS 1891.0 -> 1896.6, same frames: profiles/r06be_ab_begin_at_end.log)
+#ifndef RT_MK_MIN_RUN
+#define RT_MK_MIN_RUN 32  // samples per ticket at least, while the frame holds more than one run per lane (plan_units;
+#endif                     // 1080p at 64 spp: 16 -> 1567.5, 24 / 32 -> 1804-1808, 64 -> 1744.9, 128 -> 1664.9 Msamples/s,
+                           // profiles/r06br_ab_min_run_long.log, r06bs_ab_min_run_short.log)
 #ifndef RT_OPT_COLD
 #define RT_OPT_COLD 1  // A/B: mirror-bounce state (o, pre-bounce throughput) in LDS (LdsCold) or registers
 #endif
@@ -374,7 +378,7 @@ static void launch_mk(const DevScene& sc, const RenderArgs& a_in, double* sub_bu
                       int refill, double* tail_buf, size_t tail_cap, hipStream_t st) {
     const long blocks = resident_blocks(k_megakernel_f64<F, W>, (nsub + 255) / 256);
     RenderArgs a = a_in;
-    plan_tail(a, nsub, blocks * 256, tail_buf, tail_cap, tail_split_x2(nsub, blocks * 256), 2, 256, 32);  // plan_units
+    plan_tail(a, nsub, blocks * 256, tail_buf, tail_cap, tail_split_x2(nsub, blocks * 256), 2, 256, RT_MK_MIN_RUN);
     hipLaunchKernelGGL((k_megakernel_f64<F, W>), dim3((unsigned)blocks), dim3(256), 0, st, sc, a, sub_buf, next_sub, nsub,
                        refill);
     const long n_split = nsub - a.n_whole;
